@@ -1,0 +1,338 @@
+/*
+ * ptgs.h — C-ABI of the MI355X-native path tracer / Gaussian-splat renderer.
+ *
+ * This is the drop-in boundary for the two data-parallel hot paths of
+ * FedericoCos/PathTracer_GaussianSplatting (reference tree: /root/reference, read-only).
+ * The reference has no FFI; its hot path sits behind the Vulkan RT pipeline:
+ *   - descriptor set bindings 0-14           Vulkan_Engine/engine.cpp:2169-2224, shaders/rt_render/raytracing.glsl:109-138
+ *   - push constant RayPushConstant (80 B)   Helpers/GeneralHeaders.h:526-532
+ *   - launch vkCmdTraceRaysKHR(W, H, 1)      Vulkan_Engine/engine.cpp:1971-1976 (camera), :2789 (torus)
+ *   - per-frame protocol ubo.frame_count     Vulkan_Engine/engine.cpp:2134, :2070-2072
+ * Every struct below is byte-compatible with Helpers/GeneralHeaders.h so the reference's
+ * Engine can hand its host arrays straight to ptgs_scene_upload() and replace
+ * vkCmdTraceRaysKHR + the running-mean image with ptgs_trace_camera().
+ *
+ * Conventions:
+ *   - every entry point returns 0 (PTGS_OK) or a negative PTGS_E* code; no exceptions cross the ABI,
+ *     nothing aborts; ptgs_last_error() returns a message for the last failure on a context.
+ *   - compute entry points are stream-ordered (hipStream_t passed as void*); the caller synchronises.
+ *   - "device pointer" arguments must be device-accessible memory of the context's HIP device.
+ *   - a context is not thread-safe (thread-compatible): one host thread at a time per context.
+ */
+#ifndef PTGS_H_
+#define PTGS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTGS_ABI_VERSION 1
+
+/* ---------------- error codes ---------------- */
+#define PTGS_OK 0
+#define PTGS_EINVAL (-1)   /* bad argument / null pointer / size mismatch */
+#define PTGS_EHIP (-2)     /* HIP runtime error (allocation, launch, copy) */
+#define PTGS_ENOSCENE (-3) /* trace before ptgs_scene_upload */
+#define PTGS_ERANGE (-4)   /* size exceeds an implementation limit */
+#define PTGS_EIO (-5)      /* file could not be read/parsed (host helpers) */
+
+/* ---------------- reference struct layouts (Appendix B of SURVEY.md) ---------------- */
+
+/* Vertex, GeneralHeaders.h:65-97 / InputVertex raytracing.glsl:7-17 — 80 B */
+typedef struct ptgs_vertex {
+    float pos[3];
+    float pad1;
+    float normal[3];
+    float pad2;
+    float color[3];
+    float pad3;
+    float tangent[4];
+    float tex_coord[2];
+    float tex_coord_1[2];
+} ptgs_vertex;
+
+/* MaterialPushConstant, GeneralHeaders.h:236-269 / MaterialData raytracing.glsl:20-45 — 308 B.
+ * use_specular_glossiness_workflow is a float on the host but read as an int by the shaders
+ * (SURVEY Appendix A.2); the kernels reproduce that bit-pun. */
+typedef struct ptgs_material {
+    float base_color_factor[4];
+    float uv_normal[16];
+    float uv_emissive[16];
+    float uv_albedo[16];
+    float emissive_factor_and_pad[4];
+    float metallic_factor;
+    float roughness_factor;
+    float occlusion_strength;
+    float specular_factor;
+    float specular_color_factor[3];
+    float alpha_cutoff;
+    float transmission_factor;
+    float clearcoat_factor;
+    float clearcoat_roughness_factor;
+    float pad; /* 1.0 = is_transparent (BLEND), engine.cpp:1706 */
+    int32_t albedo_texture_index;
+    int32_t normal_texture_index;
+    int32_t metallic_roughness_texture_index;
+    int32_t emissive_texture_index;
+    int32_t occlusion_texture_index;
+    int32_t clearcoat_texture_index;
+    int32_t clearcoat_roughness_texture_index;
+    int32_t sg_id;
+    float use_specular_glossiness_workflow;
+} ptgs_material;
+
+/* UniformBufferObject, GeneralHeaders.h:300-318 (std140) — 192 B */
+typedef struct ptgs_ubo {
+    float view[16]; /* column-major (glm) */
+    float proj[16]; /* column-major, Vulkan ZO, [1][1] negated (camera.cpp:186-187) */
+    float camera_pos[3];
+    uint32_t frame_count;
+    float ambient_light[4]; /* xyz = sky radiance / 2, w = emissive-NEE scale */
+    float emissive_flux;
+    float punctual_flux;
+    float total_flux;
+    float p_emissive;
+    float fov; /* radians */
+    float height;
+    float use_lod;
+    float lod_factor;
+} ptgs_ubo;
+
+/* PunctualLight, GeneralHeaders.h:287-297 — 64 B; type 0 point, 1 directional, 2 spot */
+typedef struct ptgs_punctual_light {
+    float position[3];
+    float intensity;
+    float color[3];
+    float range;
+    float direction[3];
+    float outer_cone_cos;
+    float inner_cone_cos;
+    int32_t type;
+    float padding[2];
+} ptgs_punctual_light;
+
+/* MeshInfo GeneralHeaders.h:515-520, LightTriangle :594-597, LightCDF :599-603,
+ * PunctualLightCDF :605-609 — 16 B each */
+typedef struct ptgs_mesh_info {
+    uint32_t material_index;
+    uint32_t vertex_offset;
+    uint32_t index_offset;
+    uint32_t _pad1;
+} ptgs_mesh_info;
+
+typedef struct ptgs_light_triangle {
+    uint32_t v0, v1, v2;
+    uint32_t material_index;
+} ptgs_light_triangle;
+
+typedef struct ptgs_light_cdf {
+    float cumulative_probability;
+    uint32_t triangle_index;
+    float padding[2];
+} ptgs_light_cdf;
+
+typedef struct ptgs_punctual_cdf {
+    float cumulative_probability;
+    uint32_t light_index;
+    float padding[2];
+} ptgs_punctual_cdf;
+
+/* HitDataGPU GeneralHeaders.h:565-576 / HitData rt_datacollect/raytracing.glsl:102-108 — 48 B */
+typedef struct ptgs_hitdata {
+    float pos[3];
+    float flag;
+    float color[4];
+    float normal[3];
+    float padding;
+} ptgs_hitdata;
+
+/* RaySample GeneralHeaders.h:522-524 — 8 B */
+typedef struct ptgs_ray_sample {
+    float uv[2];
+} ptgs_ray_sample;
+
+/* RayPushConstant / PC GeneralHeaders.h:526-540 — 80 B */
+typedef struct ptgs_ray_push {
+    float model[16];
+    int32_t mode;
+    float major_radius;
+    float minor_radius;
+    float height;
+} ptgs_ray_push;
+
+/* ---------------- scene ---------------- */
+
+/* Host arrays in the reference layouts, as produced by Engine::createGlobalBindlessBuffers
+ * (engine.cpp:1658-1860). mesh_index_count[i] is the index count of the primitive behind
+ * meshes[i] (Primitive::index_count, used by buildBlas engine.cpp:545-560); the reference keeps
+ * it in the BLAS geometry, so it travels beside MeshInfo here. Meshes with fewer than 3
+ * indices are skipped exactly like buildBlas does.
+ * The context copies everything; the caller keeps ownership. */
+typedef struct ptgs_scene_desc {
+    const ptgs_vertex* vertices;
+    uint32_t num_vertices;
+    const uint32_t* indices;
+    uint32_t num_indices;
+    const ptgs_mesh_info* meshes;
+    const uint32_t* mesh_index_count;
+    uint32_t num_meshes;
+    const ptgs_material* materials;
+    uint32_t num_materials;
+    const ptgs_light_triangle* light_triangles;
+    uint32_t num_light_triangles;
+    const ptgs_light_cdf* light_cdf;
+    uint32_t num_light_cdf;
+    const ptgs_punctual_light* punctual_lights;
+    uint32_t num_punctual_lights;
+    const ptgs_punctual_cdf* punctual_cdf;
+    uint32_t num_punctual_cdf;
+    /* blue-noise texture (binding 12): RGBA32F, size x size texels, size a power of two,
+     * values already decoded with the stbi_loadf convention (RGB^2.2, A linear). */
+    const float* blue_noise_rgba32f;
+    uint32_t blue_noise_size;
+} ptgs_scene_desc;
+
+typedef struct ptgs_scene_info {
+    uint32_t num_triangles;   /* triangles in the acceleration structure */
+    uint32_t num_bvh_nodes;   /* interior nodes (each holds two child boxes) */
+    uint32_t bvh_depth;       /* max depth of the tree */
+    uint32_t max_leaf_size;
+    double build_ms;          /* host BVH build time */
+    uint64_t device_bytes;    /* bytes resident on the device for the scene */
+} ptgs_scene_info;
+
+/* ---------------- context ---------------- */
+
+typedef struct ptgs_ctx ptgs_ctx;
+
+int ptgs_create(int hip_device, ptgs_ctx** out);
+void ptgs_destroy(ptgs_ctx* ctx);
+const char* ptgs_last_error(const ptgs_ctx* ctx);
+int ptgs_abi_version(void);
+/* device the library was compiled for, e.g. "gfx950" */
+const char* ptgs_device_arch(void);
+
+/* Replaces buildBlas/initStaticTlas (engine.cpp:534-655, :1385-1520) + the descriptor uploads. */
+int ptgs_scene_upload(ptgs_ctx* ctx, const ptgs_scene_desc* desc);
+int ptgs_scene_get_info(const ptgs_ctx* ctx, ptgs_scene_info* out);
+
+/* ---------------- path tracer (raygen_camera.rgen + closesthit/miss/shadow) ---------------- */
+
+#define PTGS_ACCUM_RUNNING_MEAN 0u /* reference semantics: mix(prev, cur, 1/(frame+1)), restart at frame 0 */
+#define PTGS_ACCUM_SUM 1u          /* accum.rgb += radiance, accum.a += 1 (for sample-sharded multi-GPU) */
+
+/* Renders `spp` consecutive samples per pixel, frame counts ubo->frame_count .. +spp-1, into
+ * accum (device, W*H RGBA32F, row-major, caller-owned, read-modify-write). One call with spp=1
+ * is exactly one vkCmdTraceRaysKHR(W,H,1) of the reference (engine.cpp:1971).
+ * `frame_stride` (>=1) spaces the frame counts: sample s uses frame_count + s*frame_stride —
+ * the sample-index shard of §8e (rank g of G: frame_count=g, frame_stride=G, mode SUM). */
+int ptgs_trace_camera(ptgs_ctx* ctx, const ptgs_ubo* ubo, uint32_t width, uint32_t height,
+                      float* accum_rgba32f, uint32_t spp, uint32_t frame_stride, uint32_t accum_mode,
+                      void* hip_stream);
+
+/* Same, restricted to pixel rows [row_begin, row_end) — screen-space sharding of a frame. */
+int ptgs_trace_camera_rows(ptgs_ctx* ctx, const ptgs_ubo* ubo, uint32_t width, uint32_t height,
+                           uint32_t row_begin, uint32_t row_end, float* accum_rgba32f, uint32_t spp,
+                           uint32_t frame_stride, uint32_t accum_mode, void* hip_stream);
+
+/* Toroidal data-collection tracer (shaders/rt_datacollect/raygen.rgen:31-141): one ray per
+ * RaySample (device array, n entries), launch grid side x side with side = ceil(sqrt(n))
+ * (engine.cpp:2786), HitData running mean written in place (device array, n entries). */
+int ptgs_trace_torus(ptgs_ctx* ctx, const ptgs_ubo* ubo, const ptgs_ray_push* push,
+                     const ptgs_ray_sample* samples, uint32_t n, ptgs_hitdata* hits,
+                     void* hip_stream);
+
+/* Ray counters of the most recent trace call(s) since the last reset (device-side atomics,
+ * read back synchronously). */
+typedef struct ptgs_trace_stats {
+    uint64_t extension_rays; /* closest-hit traversals (primary + bounces) */
+    uint64_t shadow_rays;    /* any-hit traversals (NEE visibility) */
+    uint64_t samples;        /* pixel samples completed */
+    uint64_t node_visits;    /* child-box tests (only with PTGS_FLAG_COUNT_TRAVERSAL) */
+    uint64_t tri_tests;      /* ray-triangle tests (only with PTGS_FLAG_COUNT_TRAVERSAL) */
+} ptgs_trace_stats;
+
+#define PTGS_FLAG_COUNT_TRAVERSAL 1u
+int ptgs_set_flags(ptgs_ctx* ctx, uint32_t flags);
+int ptgs_stats_reset(ptgs_ctx* ctx, void* hip_stream);
+int ptgs_stats_read(ptgs_ctx* ctx, ptgs_trace_stats* out); /* synchronises the context's device */
+
+/* ---------------- rasterizers ---------------- */
+
+/* Point-cloud view (shaders/pointcloud/pointcloud.vert:44-89 + .frag:1-11; pipeline state
+ * pipeline.cpp:29-82): point i with hits[i].flag > 0 is projected by proj*view (mode 0: hit pos,
+ * mode 1: torus(u,v) + 0.01 n through push->model), drawn as a 2-px point sprite with depth test
+ * LESS against `depth` (device W*H f32, caller clears to 1.0), no blending, colour = linear
+ * hits[i].color.rgb encoded to sRGB8 into rgba8 (device W*H u32, R in the low byte). */
+int ptgs_splat_points(ptgs_ctx* ctx, const ptgs_ubo* ubo, const ptgs_ray_push* push,
+                      const ptgs_hitdata* hits, const ptgs_ray_sample* samples, uint32_t n,
+                      uint32_t width, uint32_t height, uint32_t* rgba8_srgb, float* depth,
+                      void* hip_stream);
+
+/* 3D Gaussian splatting forward (Kerbl et al. 2023; absent from the reference).
+ * SoA device arrays, N Gaussians: means xyz, scales xyz (linear, post-activation),
+ * rotations (w,x,y,z) un-normalised, opacities [0,1], colors linear RGB. */
+typedef struct ptgs_gaussians {
+    const float* means;     /* 3N */
+    const float* scales;    /* 3N */
+    const float* rotations; /* 4N */
+    const float* opacities; /* N  */
+    const float* colors;    /* 3N */
+    uint32_t count;
+} ptgs_gaussians;
+
+typedef struct ptgs_splat_stats {
+    uint32_t num_rendered; /* K = (gaussian, tile) pairs */
+    uint32_t tiles_x, tiles_y;
+    uint32_t num_visible;  /* gaussians with radius > 0 */
+} ptgs_splat_stats;
+
+/* out_rgba32f (device W*H): rgb = sum c_i a_i T_i + T_final * bg, a = 1 - T_final.
+ * Camera = ubo->view / ubo->proj (reference conventions). Tiles 16x16. Rows of tiles
+ * [tile_row_begin, tile_row_end) are rendered (full frame: 0, ~0u) — screen-tile sharding of §8e;
+ * pixels outside are left untouched. stats may be NULL (reading it synchronises the stream). */
+int ptgs_splat_gaussians(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo* ubo,
+                         uint32_t width, uint32_t height, const float bg[3],
+                         uint32_t tile_row_begin, uint32_t tile_row_end, float* out_rgba32f,
+                         ptgs_splat_stats* stats, void* hip_stream);
+
+/* Debug/parity access to the integer intermediates of the most recent ptgs_splat_gaussians call
+ * (device buffers owned by the context, valid until the next splat call):
+ * radii[N] (int32), tiles_touched[N] (u32), sorted keys[K] (u64: tile<<32 | depth bits),
+ * sorted values[K] (u32 gaussian index), tile ranges[tiles] (uint2 start,end). */
+typedef struct ptgs_splat_buffers {
+    const int32_t* radii;
+    const uint32_t* tiles_touched;
+    const uint64_t* sorted_keys;
+    const uint32_t* sorted_values;
+    const uint32_t* tile_ranges;
+    const float* means2d;   /* 2N */
+    const float* depths;    /* N */
+    const float* conic_opacity; /* 4N */
+    uint32_t num_gaussians;
+    uint32_t num_rendered;
+    uint32_t num_tiles;
+} ptgs_splat_buffers;
+int ptgs_splat_get_buffers(const ptgs_ctx* ctx, ptgs_splat_buffers* out);
+
+/* ---------------- output encode (blit rgba32f -> B8G8R8A8_SRGB, engine.cpp:2004-2020) --------- */
+/* rgba8 (device W*H u32, R in the low byte): linear -> sRGB8 of clamp(rgb,0,1), alpha 255. */
+int ptgs_encode_srgb8(ptgs_ctx* ctx, const float* rgba32f, uint32_t width, uint32_t height,
+                      uint32_t* rgba8, void* hip_stream);
+
+/* ---------------- device memory helpers (usable without any other GPU framework) ------------ */
+int ptgs_device_alloc(ptgs_ctx* ctx, size_t bytes, void** out);
+int ptgs_device_free(ptgs_ctx* ctx, void* ptr);
+int ptgs_memcpy_h2d(ptgs_ctx* ctx, void* dst, const void* src, size_t bytes);
+int ptgs_memcpy_d2h(ptgs_ctx* ctx, void* dst, const void* src, size_t bytes);
+int ptgs_memset_d32(ptgs_ctx* ctx, void* dst, uint32_t value, size_t count, void* hip_stream);
+int ptgs_synchronize(ptgs_ctx* ctx);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* PTGS_H_ */

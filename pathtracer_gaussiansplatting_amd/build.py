@@ -1,0 +1,72 @@
+"""Build the native library libptgs.so (HIP kernels for gfx950 + the C-ABI host code).
+
+Everything is compiled in-tree with hipcc so the .so travels with the repository snapshot to the
+GPU box. Flags that are part of the parity contract (see csrc/detmath.h):
+  -ffp-contract=off   no FMA contraction, so every float op rounds like the CPU oracle's
+  (no -ffast-math)    IEEE division / sqrt (gfx950: v_div_scale/fixup, v_sqrt + fixup sequences)
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+ROOT = os.path.dirname(HERE)
+INCLUDE = os.path.join(ROOT, "include")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libptgs.so")
+
+SOURCES = ["api.cpp", "bvh.cpp", "scene.cpp", "pt_kernels.hip", "raster.hip", "splat.hip"]
+ARCH = os.environ.get("PTGS_ARCH", "gfx950")
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
+          "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC]
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the HIP toolchain is required to build libptgs.so")
+
+
+def _compile(src: str) -> str:
+    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    path = os.path.join(CSRC, src)
+    deps = [path] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    deps.append(os.path.join(INCLUDE, "ptgs", "ptgs.h"))
+    if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
+        return obj
+    cmd = [_hipcc()] + COMMON + [f"--offload-arch={ARCH}", "-c", path, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [_hipcc()] + COMMON + ["-x", "hip", f"--offload-arch={ARCH}", "-c", path, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    with ThreadPoolExecutor(max_workers=min(6, os.cpu_count() or 2)) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(o) for o in objs):
+        return LIB
+    tmp = LIB + ".tmp"
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
+        "-Wl,-rpath,/opt/rocm/lib", "-L/opt/rocm/lib", "-lamdhip64"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

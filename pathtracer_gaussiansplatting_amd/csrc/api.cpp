@@ -1,0 +1,404 @@
+// api.cpp — the C-ABI boundary (include/ptgs/ptgs.h): context, scene upload, trace dispatch.
+//
+// Replaces, on the reference side (Vulkan_Engine/engine.cpp):
+//   createGlobalBindlessBuffers uploads :1658-1860 and buildBlas/initStaticTlas :534-655, :1385-1520
+//       -> ptgs_scene_upload (host BVH build + hipMemcpy of the reference-layout arrays)
+//   recordCommandBuffer's vkCmdTraceRaysKHR :1971-1976 + rt_output_image running mean
+//       -> ptgs_trace_camera
+//   torus trace :1893-1900 / :2787-2794 -> ptgs_trace_torus
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ptgs/ptgs.h"
+#include "bvh.h"
+#include "hostmath.h"
+#include "pt_launch.h"
+#include "splat.h"
+
+using namespace ptgs;
+
+struct ptgs_ctx {
+  int device = 0;
+  std::string err;
+  uint32_t flags = 0;
+  bool has_scene = false;
+  DevScene dsc{};
+  std::vector<void*> scene_allocs;
+  ptgs_scene_info info{};
+  unsigned long long* counters = nullptr;  // 8 x u64
+  SplatWorkspace* splat = nullptr;
+};
+
+namespace {
+
+int fail(ptgs_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                   \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return fail(ctx, PTGS_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+void free_scene(ptgs_ctx* c) {
+  for (void* p : c->scene_allocs) (void)hipFree(p);
+  c->scene_allocs.clear();
+  c->has_scene = false;
+  c->dsc = DevScene{};
+}
+
+template <typename T>
+int upload(ptgs_ctx* c, const T* src, size_t count, const T** dst) {
+  if (count == 0) { *dst = nullptr; return PTGS_OK; }
+  void* p = nullptr;
+  HIPCHK(c, hipMalloc(&p, count * sizeof(T)));
+  c->scene_allocs.push_back(p);
+  HIPCHK(c, hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
+  c->info.device_bytes += count * sizeof(T);
+  *dst = (const T*)p;
+  return PTGS_OK;
+}
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.devicePointer != nullptr;
+}
+
+int fill_cam(ptgs_ctx* c, const ptgs_ubo* ubo, CamParams& cp) {
+  if (!inverse4(ubo->view, cp.inv_view)) return fail(c, PTGS_EINVAL, "ubo.view is singular");
+  if (!inverse4(ubo->proj, cp.inv_proj)) return fail(c, PTGS_EINVAL, "ubo.proj is singular");
+  for (int k = 0; k < 4; ++k) cp.ambient[k] = ubo->ambient_light[k];
+  cp.emissive_flux = ubo->emissive_flux;
+  cp.punctual_flux = ubo->punctual_flux;
+  cp.p_emissive = ubo->p_emissive;
+  cp.fov = ubo->fov;
+  cp.win_height = ubo->height;
+  cp.use_lod = ubo->use_lod;
+  cp.lod_factor = ubo->lod_factor;
+  return PTGS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ptgs_abi_version(void) { return PTGS_ABI_VERSION; }
+const char* ptgs_device_arch(void) { return "gfx950"; }
+
+int ptgs_create(int hip_device, ptgs_ctx** out) {
+  if (!out) return PTGS_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) return PTGS_EHIP;
+  if (hip_device < 0 || hip_device >= n) return PTGS_EINVAL;
+  ptgs_ctx* c = new ptgs_ctx();
+  c->device = hip_device;
+  if (hipSetDevice(hip_device) != hipSuccess) { delete c; return PTGS_EHIP; }
+  if (hipMalloc(&c->counters, 8 * sizeof(unsigned long long)) != hipSuccess) { delete c; return PTGS_EHIP; }
+  if (hipMemset(c->counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess) { delete c; return PTGS_EHIP; }
+  c->splat = splat_workspace_create();
+  *out = c;
+  return PTGS_OK;
+}
+
+void ptgs_destroy(ptgs_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  free_scene(c);
+  if (c->counters) (void)hipFree(c->counters);
+  splat_workspace_destroy(c->splat);
+  delete c;
+}
+
+const char* ptgs_last_error(const ptgs_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
+  if (!c || !d) return PTGS_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!d->vertices && d->num_vertices) return fail(c, PTGS_EINVAL, "vertices is null");
+  if (!d->indices && d->num_indices) return fail(c, PTGS_EINVAL, "indices is null");
+  if (d->num_meshes && (!d->meshes || !d->mesh_index_count)) return fail(c, PTGS_EINVAL, "meshes is null");
+  if (!d->materials || d->num_materials == 0) return fail(c, PTGS_EINVAL, "at least one material is required");
+  if (!d->light_triangles || !d->light_cdf || d->num_light_cdf == 0 || d->num_light_triangles == 0)
+    return fail(c, PTGS_EINVAL, "light triangle / CDF buffers must hold >= 1 entry (engine.cpp:1766-1769 dummy)");
+  if (!d->punctual_lights || !d->punctual_cdf || d->num_punctual_lights == 0 || d->num_punctual_cdf == 0)
+    return fail(c, PTGS_EINVAL, "punctual light / CDF buffers must hold >= 1 entry (engine.cpp:1795-1797 dummy)");
+  uint32_t bn = d->blue_noise_size;
+  if (!d->blue_noise_rgba32f || bn == 0 || (bn & (bn - 1)) != 0)
+    return fail(c, PTGS_EINVAL, "blue noise must be a power-of-two square RGBA32F texture");
+
+  // gather triangles in flattening order (gid), skipping meshes with < 3 indices (engine.cpp:545-547)
+  std::vector<BuildTri> tris;
+  bool has_transparent = false;
+  for (uint32_t m = 0; m < d->num_meshes; ++m) {
+    const ptgs_mesh_info& mi = d->meshes[m];
+    uint32_t cnt = d->mesh_index_count[m];
+    if (cnt < 3) continue;
+    if (mi.material_index >= d->num_materials) return fail(c, PTGS_EINVAL, "mesh %u: material %u out of range", m, mi.material_index);
+    if ((uint64_t)mi.index_offset + cnt > d->num_indices) return fail(c, PTGS_EINVAL, "mesh %u: index range out of bounds", m);
+    const ptgs_material& mat = d->materials[mi.material_index];
+    uint32_t flags = (mat.pad > 0.5f) ? 1u : 0u;  // non-opaque geometry (engine.cpp:562-567)
+    has_transparent |= flags != 0;
+    for (uint32_t p = 0; p < cnt / 3; ++p) {
+      BuildTri t;
+      for (int k = 0; k < 3; ++k) {
+        uint32_t vi = d->indices[mi.index_offset + 3 * p + k] + mi.vertex_offset;
+        if (vi >= d->num_vertices) return fail(c, PTGS_EINVAL, "mesh %u prim %u: vertex %u out of range", m, p, vi);
+        float* dst = k == 0 ? t.v0 : (k == 1 ? t.v1 : t.v2);
+        std::memcpy(dst, d->vertices[vi].pos, 12);
+      }
+      t.mesh = m; t.prim = p; t.gid = (uint32_t)tris.size(); t.flags = flags;
+      tris.push_back(t);
+    }
+  }
+  if (tris.size() >= (1u << 27)) return fail(c, PTGS_ERANGE, "too many triangles (%zu)", tris.size());
+  if (d->num_punctual_cdf < d->num_punctual_lights)
+    return fail(c, PTGS_EINVAL, "punctual CDF shorter than the light list (binary search runs over the light count)");
+  for (uint32_t i = 0; i < d->num_light_cdf; ++i)
+    if (d->light_cdf[i].triangle_index >= d->num_light_triangles)
+      return fail(c, PTGS_EINVAL, "light CDF entry %u: triangle %u out of range", i, d->light_cdf[i].triangle_index);
+  for (uint32_t i = 0; i < d->num_light_triangles; ++i) {
+    const ptgs_light_triangle& lt = d->light_triangles[i];
+    if (d->num_vertices == 0 || lt.v0 >= d->num_vertices || lt.v1 >= d->num_vertices || lt.v2 >= d->num_vertices) {
+      if (d->num_light_triangles == 1 && lt.v0 == 0 && lt.v1 == 0 && lt.v2 == 0) continue;  // dummy
+      return fail(c, PTGS_EINVAL, "light triangle %u references a vertex out of range", i);
+    }
+  }
+
+  auto t0 = std::chrono::steady_clock::now();
+  BvhOut bvh;
+  build_bvh(tris, 4, bvh);
+  auto t1 = std::chrono::steady_clock::now();
+  if (bvh.depth >= PTGS_STACK - 1) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
+
+  free_scene(c);
+  c->info = ptgs_scene_info{};
+  DevScene s{};
+  int rc;
+  if ((rc = upload(c, (const float4*)bvh.nodes.data(), bvh.nodes.size() / 4, &s.nodes))) return rc;
+  if ((rc = upload(c, (const float4*)bvh.tris.data(), bvh.tris.size() / 4, &s.tris))) return rc;
+  if ((rc = upload(c, bvh.tri_flags.data(), bvh.tri_flags.size(), &s.tri_flags))) return rc;
+  // a zero vertex/index count still needs valid (never dereferenced) pointers
+  ptgs_vertex dummy_v{};
+  uint32_t dummy_i = 0;
+  ptgs_mesh_info dummy_m{};
+  if ((rc = upload(c, d->num_vertices ? d->vertices : &dummy_v, d->num_vertices ? d->num_vertices : 1, &s.vertices))) return rc;
+  if ((rc = upload(c, d->num_indices ? d->indices : &dummy_i, d->num_indices ? d->num_indices : 1, &s.indices))) return rc;
+  if ((rc = upload(c, d->num_meshes ? d->meshes : &dummy_m, d->num_meshes ? d->num_meshes : 1, &s.meshes))) return rc;
+  if ((rc = upload(c, d->materials, d->num_materials, &s.materials))) return rc;
+  if ((rc = upload(c, d->light_triangles, d->num_light_triangles, &s.light_tris))) return rc;
+  if ((rc = upload(c, d->light_cdf, d->num_light_cdf, &s.light_cdf))) return rc;
+  if ((rc = upload(c, d->punctual_lights, d->num_punctual_lights, &s.plights))) return rc;
+  if ((rc = upload(c, d->punctual_cdf, d->num_punctual_cdf, &s.pcdf))) return rc;
+  if ((rc = upload(c, (const float4*)d->blue_noise_rgba32f, (size_t)bn * bn, &s.blue_noise))) return rc;
+  s.num_light_cdf = d->num_light_cdf;
+  s.num_plights = d->num_punctual_lights;
+  s.bn_size = (int32_t)bn;
+  s.has_transparent = has_transparent ? 1 : 0;
+  c->dsc = s;
+  c->has_scene = true;
+  c->info.num_triangles = (uint32_t)tris.size();
+  c->info.num_bvh_nodes = bvh.num_nodes;
+  c->info.bvh_depth = bvh.depth;
+  c->info.max_leaf_size = bvh.max_leaf;
+  c->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  return PTGS_OK;
+}
+
+int ptgs_scene_get_info(const ptgs_ctx* c, ptgs_scene_info* out) {
+  if (!c || !out) return PTGS_EINVAL;
+  if (!c->has_scene) return PTGS_ENOSCENE;
+  *out = c->info;
+  return PTGS_OK;
+}
+
+int ptgs_trace_camera_rows(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_t h, uint32_t row_begin,
+                           uint32_t row_end, float* accum, uint32_t spp, uint32_t frame_stride,
+                           uint32_t accum_mode, void* stream) {
+  if (!c || !ubo || !accum) return fail(c, PTGS_EINVAL, "null argument");
+  if (!c->has_scene) return fail(c, PTGS_ENOSCENE, "no scene uploaded");
+  if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
+  if (row_end > h) row_end = h;
+  if (row_begin > row_end) return fail(c, PTGS_EINVAL, "bad row range");
+  if (frame_stride == 0) return fail(c, PTGS_EINVAL, "frame_stride must be >= 1");
+  if (accum_mode > PTGS_ACCUM_SUM) return fail(c, PTGS_EINVAL, "bad accum mode");
+  if (!is_device_ptr(accum)) return fail(c, PTGS_EINVAL, "accum is not a device pointer");
+  HIPCHK(c, hipSetDevice(c->device));
+  CamParams cp;
+  int rc = fill_cam(c, ubo, cp);
+  if (rc) return rc;
+  hipError_t e = launch_pt_camera(c->dsc, cp, accum, w, h, row_begin, row_end, spp, ubo->frame_count, frame_stride,
+                                  accum_mode, c->counters, (c->flags & PTGS_FLAG_COUNT_TRAVERSAL) != 0,
+                                  (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "pt_camera launch: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
+int ptgs_trace_camera(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_t h, float* accum, uint32_t spp,
+                      uint32_t frame_stride, uint32_t accum_mode, void* stream) {
+  return ptgs_trace_camera_rows(c, ubo, w, h, 0, h, accum, spp, frame_stride, accum_mode, stream);
+}
+
+int ptgs_trace_torus(ptgs_ctx* c, const ptgs_ubo* ubo, const ptgs_ray_push* push, const ptgs_ray_sample* samples,
+                     uint32_t n, ptgs_hitdata* hits, void* stream) {
+  if (!c || !ubo || !push) return fail(c, PTGS_EINVAL, "null argument");
+  if (!c->has_scene) return fail(c, PTGS_ENOSCENE, "no scene uploaded");
+  if (n == 0) return PTGS_OK;
+  if (!is_device_ptr(samples) || !is_device_ptr(hits)) return fail(c, PTGS_EINVAL, "samples/hits must be device pointers");
+  HIPCHK(c, hipSetDevice(c->device));
+  CamParams cp;
+  int rc = fill_cam(c, ubo, cp);
+  if (rc) return rc;
+  TorusParams tp;
+  std::memcpy(tp.model, push->model, sizeof(tp.model));
+  tp.major_radius = push->major_radius;
+  tp.minor_radius = push->minor_radius;
+  tp.height = push->height;
+  // side = ceil(sqrt(n)) (engine.cpp:2786)
+  uint32_t side = (uint32_t)std::ceil(std::sqrt((double)n));
+  while ((uint64_t)side * side < n) side++;
+  hipError_t e = launch_pt_torus(c->dsc, cp, tp, samples, n, side, ubo->frame_count, hits, c->counters,
+                                 (c->flags & PTGS_FLAG_COUNT_TRAVERSAL) != 0, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "pt_torus launch: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
+int ptgs_set_flags(ptgs_ctx* c, uint32_t flags) {
+  if (!c) return PTGS_EINVAL;
+  c->flags = flags;
+  return PTGS_OK;
+}
+
+int ptgs_stats_reset(ptgs_ctx* c, void* stream) {
+  if (!c) return PTGS_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), (hipStream_t)stream));
+  return PTGS_OK;
+}
+
+int ptgs_stats_read(ptgs_ctx* c, ptgs_trace_stats* out) {
+  if (!c || !out) return PTGS_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipDeviceSynchronize());
+  unsigned long long v[8];
+  HIPCHK(c, hipMemcpy(v, c->counters, sizeof(v), hipMemcpyDeviceToHost));
+  out->extension_rays = v[0];
+  out->shadow_rays = v[1];
+  out->samples = v[2];
+  out->node_visits = v[3];
+  out->tri_tests = v[4];
+  return PTGS_OK;
+}
+
+int ptgs_device_alloc(ptgs_ctx* c, size_t bytes, void** out) {
+  if (!c || !out) return PTGS_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMalloc(out, bytes ? bytes : 16));
+  return PTGS_OK;
+}
+int ptgs_device_free(ptgs_ctx* c, void* p) {
+  if (!c) return PTGS_EINVAL;
+  HIPCHK(c, hipFree(p));
+  return PTGS_OK;
+}
+int ptgs_memcpy_h2d(ptgs_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (!c) return PTGS_EINVAL;
+  HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return PTGS_OK;
+}
+int ptgs_memcpy_d2h(ptgs_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (!c) return PTGS_EINVAL;
+  HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return PTGS_OK;
+}
+int ptgs_memset_d32(ptgs_ctx* c, void* dst, uint32_t value, size_t count, void* stream) {
+  if (!c) return PTGS_EINVAL;
+  HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)dst, (int)value, count, (hipStream_t)stream));
+  return PTGS_OK;
+}
+int ptgs_synchronize(ptgs_ctx* c) {
+  if (!c) return PTGS_EINVAL;
+  HIPCHK(c, hipDeviceSynchronize());
+  return PTGS_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// rasterizers
+// ---------------------------------------------------------------------------------------------
+#include "raster.h"
+
+extern "C" {
+
+int ptgs_splat_gaussians(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
+                         const float bg[3], uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
+                         ptgs_splat_stats* stats, void* stream) {
+  if (!c || !g || !ubo || !out || !bg) return fail(c, PTGS_EINVAL, "null argument");
+  if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
+  if (g->count && (!is_device_ptr(g->means) || !is_device_ptr(g->scales) || !is_device_ptr(g->rotations) ||
+                   !is_device_ptr(g->opacities) || !is_device_ptr(g->colors)))
+    return fail(c, PTGS_EINVAL, "gaussian arrays must be device pointers");
+  if (!is_device_ptr(out)) return fail(c, PTGS_EINVAL, "out is not a device pointer");
+  if (ubo->proj[0] == 0.0f || ubo->proj[5] == 0.0f) return fail(c, PTGS_EINVAL, "degenerate projection");
+  HIPCHK(c, hipSetDevice(c->device));
+  float mvp[16];
+  mat4_mul(ubo->proj, ubo->view, mvp);
+  hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, tile_row_begin,
+                                 tile_row_end, out, stats, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_gaussians: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
+int ptgs_splat_get_buffers(const ptgs_ctx* c, ptgs_splat_buffers* out) {
+  if (!c || !out) return PTGS_EINVAL;
+  splat_get_buffers(c->splat, out);
+  return PTGS_OK;
+}
+
+int ptgs_splat_points(ptgs_ctx* c, const ptgs_ubo* ubo, const ptgs_ray_push* push, const ptgs_hitdata* hits,
+                      const ptgs_ray_sample* samples, uint32_t n, uint32_t w, uint32_t h, uint32_t* rgba8,
+                      float* depth, void* stream) {
+  if (!c || !ubo || !push || !rgba8 || !depth) return fail(c, PTGS_EINVAL, "null argument");
+  if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
+  if (n && (!is_device_ptr(hits) || (push->mode == 1 && !is_device_ptr(samples))))
+    return fail(c, PTGS_EINVAL, "hits/samples must be device pointers");
+  if (!is_device_ptr(rgba8) || !is_device_ptr(depth)) return fail(c, PTGS_EINVAL, "rgba8/depth must be device pointers");
+  HIPCHK(c, hipSetDevice(c->device));
+  float mvp[16];
+  mat4_mul(ubo->proj, ubo->view, mvp);
+  unsigned long long* keys = nullptr;
+  HIPCHK(c, splat_point_keys(c->splat, (size_t)w * h, &keys));
+  hipError_t e = launch_splat_points(mvp, push->model, push->major_radius, push->minor_radius, push->height,
+                                     push->mode, hits, samples, n, w, h, keys, depth, rgba8, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_points: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
+int ptgs_encode_srgb8(ptgs_ctx* c, const float* rgba32f, uint32_t w, uint32_t h, uint32_t* rgba8, void* stream) {
+  if (!c || !rgba32f || !rgba8) return fail(c, PTGS_EINVAL, "null argument");
+  if (!is_device_ptr(rgba32f) || !is_device_ptr(rgba8)) return fail(c, PTGS_EINVAL, "buffers must be device pointers");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipError_t e = launch_encode_srgb8(rgba32f, rgba8, w * h, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "encode_srgb8: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,525 @@
+// pt_device.h — device-side path-tracing stages for gfx950.
+//
+// What the Vulkan RT pipeline of the reference does in shaders + fixed function, restated as
+// plain HIP device code:
+//   traversal  : software BVH2 walk (the reference uses the driver's HW traversal,
+//                raygen_camera.rgen:51 / closesthit.rchit:115,124; gfx950 has no BVH instruction,
+//                SURVEY.md §0.6) — closest hit with a deterministic tie-break (equal t -> lower
+//                triangle id), any-hit for shadow rays.
+//   closest_hit: shaders/rt_render/closesthit.rchit:324-621 (+ NEE helpers :113-320)
+//   miss       : shaders/rt_render/miss.rmiss:9-14, shadow.rmiss:9-11
+//   rnd        : shaders/rt_render/raytracing.glsl:141-146
+// All float math goes through detmath.h so results are bit-identical to the CPU oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include "detmath.h"
+#include "../../include/ptgs/ptgs.h"
+
+namespace ptgs {
+
+// ---------------------------------------------------------------------------------------------
+// Device scene (layouts chosen for gfx950: 16-B aligned float4 records, one node = 64 B = half a
+// 128-B cache line, triangles pre-gathered as (v0, e1, e2) so traversal never touches the 80-B
+// reference vertices).
+// ---------------------------------------------------------------------------------------------
+struct DevScene {
+  const float4* nodes;            // 4 float4 per interior node (see bvh.h)
+  const float4* tris;             // 3 float4 per triangle: (v0, mesh_bits) (e1, prim_bits) (e2, gid_bits)
+  const uint32_t* tri_flags;      // bit0: non-opaque (any-hit shader runs)
+  const ptgs_vertex* vertices;
+  const uint32_t* indices;
+  const ptgs_mesh_info* meshes;
+  const ptgs_material* materials;
+  const ptgs_light_triangle* light_tris;
+  const ptgs_light_cdf* light_cdf;
+  const ptgs_punctual_light* plights;
+  const ptgs_punctual_cdf* pcdf;
+  const float4* blue_noise;
+  uint32_t num_light_cdf;
+  uint32_t num_plights;
+  int32_t bn_size;
+  int32_t has_transparent;
+};
+
+// UBO fields the shaders read (raytracing.glsl:111-125), with the two matrix inverses the
+// ray-gen computes per pixel (raygen_camera.rgen:32-34) precomputed once on the host.
+struct CamParams {
+  float inv_view[16];
+  float inv_proj[16];
+  float ambient[4];
+  float emissive_flux, punctual_flux, p_emissive;
+  float fov, win_height, use_lod, lod_factor;
+};
+
+struct Hit {
+  float t, u, v;
+  uint32_t gid;   // global triangle id (flattening order), 0xffffffff = miss
+  uint32_t slot;  // triangle record index in BVH order (mesh/prim are re-fetched from it)
+};
+
+struct TraversalCounters {
+  uint32_t nodes;
+  uint32_t tris;
+};
+
+#define PTGS_STACK 64
+
+PTGS_HD float i2f(int x) { union { int i; float f; } c; c.i = x; return c.f; }
+__device__ __forceinline__ int f2i(float x) { return __float_as_int(x); }
+__device__ __forceinline__ uint32_t f2u(float x) { return __float_as_uint(x); }
+
+// PCG hash, raytracing.glsl:141-146
+__device__ __forceinline__ float rnd(uint32_t& state) {
+  uint32_t prev = state;
+  state = prev * 747796405u + 2891336453u;
+  uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+  return (float)((word >> 22u) ^ word) / 4294967296.0f;
+}
+
+// Stateless hash used for stochastic (BLEND) any-hit decisions: the reference draws
+// rnd(payload.seed) per candidate hit in driver traversal order (alpha.rahit:58), which no
+// software traversal can reproduce; we hash (seed, triangle) instead (documented deviation).
+__device__ __forceinline__ float alpha_hash(uint32_t seed, uint32_t gid) {
+  uint32_t s = seed ^ (gid * 0x9E3779B9u);
+  return rnd(s);
+}
+
+__device__ __forceinline__ v3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+
+// ---------------------------------------------------------------------------------------------
+// Ray / box / triangle
+// ---------------------------------------------------------------------------------------------
+struct Ray {
+  v3 o, d, inv;
+  float tmin, tmax;
+};
+
+__device__ __forceinline__ float safe_inv(float d) {
+  const float eps = 1e-20f;
+  float a = absx(d) < eps ? (d < 0.0f ? -eps : eps) : d;
+  return 1.0f / a;
+}
+
+__device__ __forceinline__ Ray make_ray(v3 o, v3 d, float tmin, float tmax) {
+  Ray r; r.o = o; r.d = d; r.tmin = tmin; r.tmax = tmax;
+  r.inv = mk3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  return r;
+}
+
+// Slab test on the two child boxes of one node. Boxes are padded on the host (bvh.cpp) so the
+// test is conservative w.r.t. the triangle test's rounding.
+__device__ __forceinline__ void box2(const Ray& r, float4 n0, float4 n1, float4 n2, float tcap,
+                                     bool& h0, bool& h1, float& t0, float& t1) {
+  float ax0 = (n0.x - r.o.x) * r.inv.x, ax1 = (n0.y - r.o.x) * r.inv.x;
+  float ay0 = (n0.z - r.o.y) * r.inv.y, ay1 = (n0.w - r.o.y) * r.inv.y;
+  float az0 = (n2.x - r.o.z) * r.inv.z, az1 = (n2.y - r.o.z) * r.inv.z;
+  float bx0 = (n1.x - r.o.x) * r.inv.x, bx1 = (n1.y - r.o.x) * r.inv.x;
+  float by0 = (n1.z - r.o.y) * r.inv.y, by1 = (n1.w - r.o.y) * r.inv.y;
+  float bz0 = (n2.z - r.o.z) * r.inv.z, bz1 = (n2.w - r.o.z) * r.inv.z;
+  float an = fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fmaxf(fminf(az0, az1), r.tmin));
+  float af = fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fminf(fmaxf(az0, az1), tcap));
+  float bn = fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fmaxf(fminf(bz0, bz1), r.tmin));
+  float bf = fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fminf(fmaxf(bz0, bz1), tcap));
+  h0 = an <= af * 1.0000004f;
+  h1 = bn <= bf * 1.0000004f;
+  t0 = an; t1 = bn;
+}
+
+// Moller-Trumbore, double-sided (TriangleFacingCullDisable, engine.cpp:1460). Operation order is
+// part of the parity contract with the oracle (oracle/ptgs_oracle.c: tri_intersect).
+__device__ __forceinline__ bool tri_isect(const Ray& r, v3 v0, v3 e1, v3 e2, float& t, float& u, float& v) {
+  v3 pvec = cross3(r.d, e2);
+  float det = dot3(e1, pvec);
+  if (det == 0.0f) return false;
+  float inv_det = 1.0f / det;
+  v3 tvec = r.o - v0;
+  u = dot3(tvec, pvec) * inv_det;
+  if (u < 0.0f || u > 1.0f) return false;
+  v3 qvec = cross3(tvec, e1);
+  v = dot3(r.d, qvec) * inv_det;
+  if (v < 0.0f || u + v > 1.0f) return false;
+  t = dot3(e2, qvec) * inv_det;
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Materials / any-hit (alpha.rahit:14-61, untextured alpha = base_color_factor.a)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool anyhit_accept(const DevScene& sc, uint32_t mesh, uint32_t seed, uint32_t gid) {
+  const ptgs_material& m = sc.materials[sc.meshes[mesh].material_index];
+  float alpha_cutoff = m.alpha_cutoff;
+  bool is_blend = m.pad > 0.5f;
+  if (alpha_cutoff == 0.0f && !is_blend) return true;
+  float alpha = m.base_color_factor[3];
+  if (alpha_cutoff > 0.0f) return !(alpha < alpha_cutoff);
+  return !(alpha_hash(seed, gid) > alpha);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Traversal
+// ---------------------------------------------------------------------------------------------
+template <bool STATS>
+__device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, int leaf, Hit& h,
+                                             uint32_t seed, TraversalCounters& cnt) {
+  uint32_t L = (uint32_t)(~leaf);
+  uint32_t start = L & 0x07ffffffu;
+  uint32_t count = (L >> 27) + 1u;
+  for (uint32_t k = 0; k < count; ++k) {
+    const float4* tp = sc.tris + 3u * (start + k);
+    float4 a = tp[0], b = tp[1], c = tp[2];
+    if (STATS) cnt.tris++;
+    float t, u, v;
+    if (!tri_isect(r, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), t, u, v)) continue;
+    if (!(t >= r.tmin && t <= h.t)) continue;
+    uint32_t gid = f2u(c.w);
+    if (t == h.t && gid >= h.gid) continue;
+    if (sc.has_transparent && (sc.tri_flags[start + k] & 1u)) {
+      if (!anyhit_accept(sc, f2u(a.w), seed, gid)) continue;
+    }
+    h.t = t; h.u = u; h.v = v; h.gid = gid; h.slot = start + k;
+  }
+}
+
+template <bool STATS>
+__device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, uint32_t seed, TraversalCounters& cnt) {
+  Hit h; h.t = r.tmax; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu; h.slot = 0;
+  int stack[PTGS_STACK];
+  int sp = 0;
+  int node = 0;
+  while (true) {
+    while (node >= 0) {
+      const float4* np = sc.nodes + 4 * node;
+      float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+      bool h0, h1; float t0, t1;
+      box2(r, n0, n1, n2, h.t, h0, h1, t0, t1);
+      if (STATS) cnt.nodes += 2;
+      int c0 = f2i(n3.x), c1 = f2i(n3.y);
+      if (h0 && h1) {
+        int near = c0, far = c1;
+        if (t1 < t0) { near = c1; far = c0; }
+        stack[sp++] = far;
+        node = near;
+      } else if (h0) {
+        node = c0;
+      } else if (h1) {
+        node = c1;
+      } else {
+        if (sp == 0) return h;
+        node = stack[--sp];
+      }
+    }
+    leaf_closest<STATS>(sc, r, node, h, seed, cnt);
+    if (sp == 0) return h;
+    node = stack[--sp];
+  }
+}
+
+// any-hit: true if something blocks the segment [tmin, tmax]
+template <bool STATS>
+__device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint32_t seed, TraversalCounters& cnt) {
+  int stack[PTGS_STACK];
+  int sp = 0;
+  int node = 0;
+  while (true) {
+    while (node >= 0) {
+      const float4* np = sc.nodes + 4 * node;
+      float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+      bool h0, h1; float t0, t1;
+      box2(r, n0, n1, n2, r.tmax, h0, h1, t0, t1);
+      if (STATS) cnt.nodes += 2;
+      int c0 = f2i(n3.x), c1 = f2i(n3.y);
+      if (h0 && h1) {
+        int near = c0, far = c1;
+        if (t1 < t0) { near = c1; far = c0; }
+        stack[sp++] = far;
+        node = near;
+      } else if (h0) {
+        node = c0;
+      } else if (h1) {
+        node = c1;
+      } else {
+        if (sp == 0) return false;
+        node = stack[--sp];
+      }
+    }
+    uint32_t L = (uint32_t)(~node);
+    uint32_t start = L & 0x07ffffffu;
+    uint32_t count = (L >> 27) + 1u;
+    for (uint32_t k = 0; k < count; ++k) {
+      const float4* tp = sc.tris + 3u * (start + k);
+      float4 a = tp[0], b = tp[1], c = tp[2];
+      if (STATS) cnt.tris++;
+      float t, u, v;
+      if (!tri_isect(r, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), t, u, v)) continue;
+      if (!(t >= r.tmin && t <= r.tmax)) continue;
+      if (sc.has_transparent && (sc.tri_flags[start + k] & 1u)) {
+        if (!anyhit_accept(sc, f2u(a.w), seed, f2u(c.w))) continue;
+      }
+      return true;
+    }
+    if (sp == 0) return false;
+    node = stack[--sp];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Payload (raytracing.glsl:90-100; rt_datacollect adds hit_pos/normal)
+// ---------------------------------------------------------------------------------------------
+struct Payload {
+  v3 color;
+  v3 next_o;
+  v3 next_d;
+  float hit_flag;
+  v3 weight;
+  uint32_t seed;
+  float last_pdf;
+  v2 blue;
+  int depth;
+  v3 hit_pos;
+  v3 normal;
+};
+
+struct ShadeCtx {
+  const DevScene* sc;
+  const CamParams* cp;
+  uint32_t shadow_rays;
+};
+
+#define PT_PI 3.14159265359f
+#define PT_PHI 1.61803398875f
+
+// closesthit.rchit:16-19
+__device__ __forceinline__ float blue_noise_dim(const Payload& p, int dim) {
+  float base = (dim % 2 == 0) ? p.blue.x : p.blue.y;
+  return fractx((base + ((float)p.depth * PT_PHI)) + ((float)dim * 0.754877f));
+}
+
+__device__ __forceinline__ v3 safe_normalize(v3 v) {
+  float len = length3(v);
+  return (len < 1e-6f) ? mk3(0.0f, 1.0f, 0.0f) : v / len;
+}
+
+// closesthit.rchit:49-51
+__device__ __forceinline__ v3 f_schlick(float cos_theta, v3 f0) {
+  float p = pow5(clampf(1.0f - cos_theta, 0.0f, 1.0f));
+  return f0 + (1.0f - f0) * p;
+}
+
+// :54-58
+__device__ __forceinline__ void ortho_basis(v3 n, v3& t, v3& b) {
+  v3 up = absx(n.z) < 0.999f ? mk3(0.f, 0.f, 1.f) : mk3(1.f, 0.f, 0.f);
+  t = safe_normalize(cross3(up, n));
+  b = cross3(n, t);
+}
+
+// :60-69
+__device__ __forceinline__ v3 sample_cosine(const Payload& p, v3 n) {
+  float r1 = blue_noise_dim(p, 0);
+  float r2 = blue_noise_dim(p, 1);
+  float phi = (2.0f * PT_PI) * r1;
+  float sq = sqrtx(r2);
+  float s, c; sincosx(phi, &s, &c);
+  v3 local = mk3(c * sq, s * sq, sqrtx(1.0f - r2));
+  v3 t, b; ortho_basis(n, t, b);
+  return safe_normalize((t * local.x + b * local.y) + n * local.z);
+}
+
+// :71-78
+__device__ __forceinline__ float d_ggx(v3 n, v3 h, float roughness) {
+  float a = roughness * roughness;
+  float a2 = a * a;
+  float ndh = fmaxx(dot3(n, h), 0.0f);
+  float ndh2 = ndh * ndh;
+  float denom = ndh2 * (a2 - 1.0f) + 1.0f;
+  return a2 / (((PT_PI * denom) * denom) + 0.0001f);
+}
+
+// :80-85
+__device__ __forceinline__ float v_smith(float ndv, float ndl, float roughness) {
+  float a = roughness * roughness;
+  float ggxv = ndl * (ndv * (1.0f - a) + a);
+  float ggxl = ndv * (ndl * (1.0f - a) + a);
+  return 0.5f / fmaxx(ggxv + ggxl, 0.0001f);
+}
+
+// :87-99 (dims 2,3)
+__device__ __forceinline__ v3 sample_ggx(const Payload& p, v3 n, float roughness) {
+  float r1 = blue_noise_dim(p, 2);
+  float r2 = blue_noise_dim(p, 3);
+  float a = roughness * roughness;
+  float phi = (2.0f * PT_PI) * r1;
+  float denom = 1.0f + (a * a - 1.0f) * r2;
+  float cos_t = sqrtx((1.0f - r2) / fmaxx(denom, 0.0001f));
+  float sin_t = sqrtx(1.0f - cos_t * cos_t);
+  float s, c; sincosx(phi, &s, &c);
+  v3 hl = mk3(sin_t * c, sin_t * s, cos_t);
+  v3 t, b; ortho_basis(n, t, b);
+  return safe_normalize((t * hl.x + b * hl.y) + n * hl.z);
+}
+
+// :101-107
+__device__ __forceinline__ float pdf_ggx(v3 n, v3 v, v3 l, float roughness) {
+  v3 h = safe_normalize(v + l);
+  float ndh = fmaxx(dot3(n, h), 0.0f);
+  float vdh = fmaxx(dot3(v, h), 0.0f);
+  float dn = d_ggx(n, h, roughness) * ndh;
+  return dn / (4.0f * vdh + 0.0001f);
+}
+
+// :109-111
+__device__ __forceinline__ float pdf_lambert(v3 n, v3 l) { return fmaxx(dot3(n, l), 0.0f) / PT_PI; }
+
+template <bool STATS>
+__device__ __forceinline__ float trace_shadow_dist(ShadeCtx& c, v3 o, v3 d, float maxd, uint32_t seed, TraversalCounters& cnt) {
+  c.shadow_rays++;
+  Ray r = make_ray(o, d, 0.001f, maxd);
+  return trace_any<STATS>(*c.sc, r, seed, cnt) ? 0.0f : 1.0f;
+}
+
+// :119-126
+template <bool STATS>
+__device__ __forceinline__ float trace_shadow(ShadeCtx& c, v3 o, v3 light_pos, uint32_t seed, TraversalCounters& cnt) {
+  v3 l = light_pos - o;
+  float dist = length3(l);
+  l = safe_normalize(l);
+  return trace_shadow_dist<STATS>(c, o, l, dist - 0.005f, seed, cnt);
+}
+
+// binary search over a CDF (closesthit.rchit:131-137 / :197-203 / :262-268)
+template <typename CDF>
+__device__ __forceinline__ uint32_t cdf_search(const CDF* cdf, uint32_t n, float r) {
+  uint32_t idx = 0, left = 0, right = n;
+  while (left < right) {
+    uint32_t mid = (left + right) >> 1;
+    if (cdf[mid].cumulative_probability < r) left = mid + 1;
+    else { idx = mid; right = mid; }
+  }
+  return idx;
+}
+
+// :128-192
+template <bool STATS>
+__device__ void sample_punctual(ShadeCtx& c, const Payload& p, v3 hit_pos, v3 n, v3 n_geo, v3 v, v3 albedo,
+                                float roughness, v3 f0, float transmission, v3& lo, TraversalCounters& cnt) {
+  const DevScene& sc = *c.sc;
+  uint32_t num_lights = sc.num_plights;
+  float r_select = blue_noise_dim(p, 4);
+  uint32_t li = cdf_search(sc.pcdf, num_lights, r_select);
+  const ptgs_punctual_light& light = sc.plights[li];
+  v3 l;
+  float attenuation = 1.0f;
+  v3 lpos = ld3(light.position);
+  v3 ldir = ld3(light.direction);
+  if (light.type == 1) {
+    l = normalize3(-ldir);
+    attenuation = 1.0f;
+  } else {
+    v3 off = lpos - hit_pos;
+    float dist_sq = dot3(off, off);
+    dist_sq = fmaxx(dist_sq, 0.01f);
+    float dist = sqrtx(dist_sq);
+    l = off / dist;
+    attenuation = 1.0f / dist_sq;
+    if (light.range > 0.0f) {
+      float ra = fmaxx(fminx(1.0f - pow4(dist / light.range), 1.0f), 0.0f) / dist_sq;
+      attenuation = ra / dist_sq;
+    }
+    if (light.type == 2) {
+      float cos_dir = dot3(-l, normalize3(ldir));
+      float spot_scale = 1.0f / fmaxx(light.inner_cone_cos - light.outer_cone_cos, 0.001f);
+      float spot_offset = -light.outer_cone_cos * spot_scale;
+      float sa = clampf(cos_dir * spot_scale + spot_offset, 0.0f, 1.0f);
+      attenuation = attenuation * (sa * sa);
+    }
+  }
+  v3 le = (ld3(light.color) * light.intensity) * attenuation;
+  float ndl = fmaxx(dot3(n, l), 0.0f);
+  if (ndl < 0.001f) return;
+  if (ndl > 0.0f && length3(le) > 0.0f) {
+    v3 so = hit_pos + n_geo * 0.001f;
+    float vis;
+    if (light.type == 1) vis = trace_shadow_dist<STATS>(c, so, l, 10000.0f, p.seed, cnt);
+    else vis = trace_shadow<STATS>(c, so, lpos, p.seed, cnt);
+    vis = fmaxx(vis, transmission);
+    if (vis > 0.0f) {
+      float weight = (float)num_lights;
+      v3 h = safe_normalize(v + l);
+      float ndf = d_ggx(n, h, roughness);
+      float vis_t = v_smith(dot3(n, v), ndl, roughness);
+      v3 f = f_schlick(dot3(h, v), f0);
+      v3 kd = (mk3(1.0f) - f) * (1.0f - transmission);
+      v3 spec = f * (ndf * vis_t);
+      v3 diff = ((kd * albedo) / PT_PI) * (1.0f - transmission);
+      lo = lo + ((((diff + spec) * le) * ndl) * vis) * weight;
+    }
+  }
+}
+
+// :194-257 (sg == true) and :259-320 (sg == false)
+template <bool STATS>
+__device__ void sample_emissive(ShadeCtx& c, const Payload& p, bool sg, v3 hit_pos, v3 n, v3 n_geo, v3 v,
+                                v3 albedo, float roughness, float metallic, v3 f0, float transmission, v3& lo,
+                                TraversalCounters& cnt) {
+  const DevScene& sc = *c.sc;
+  uint32_t num = sc.num_light_cdf;
+  float r_select = blue_noise_dim(p, sg ? 4 : 7);
+  uint32_t idx = cdf_search(sc.light_cdf, num, r_select);
+  uint32_t tri_idx = sc.light_cdf[idx].triangle_index;
+  ptgs_light_triangle tri = sc.light_tris[tri_idx];
+  v3 p0 = ld3(sc.vertices[tri.v0].pos);
+  v3 p1 = ld3(sc.vertices[tri.v1].pos);
+  v3 p2 = ld3(sc.vertices[tri.v2].pos);
+  float u = blue_noise_dim(p, sg ? 5 : 8);
+  float w = blue_noise_dim(p, sg ? 6 : 9);
+  if (u + w > 1.0f) { u = 1.0f - u; w = 1.0f - w; }
+  v3 lp = (p0 * ((1.0f - u) - w) + p1 * u) + p2 * w;
+  v3 cr = cross3(p1 - p0, p2 - p0);
+  v3 ln = sg ? normalize3(cr) : safe_normalize(cr);
+  v3 l = lp - hit_pos;
+  float dist_sq = dot3(l, l);
+  dist_sq = fmaxx(dist_sq, 0.0001f);
+  float dist = sqrtx(dist_sq);
+  l = l / dist;
+  float ndl = fmaxx(dot3(n, l), 0.0f);
+  if (ndl < 0.001f) return;
+  float ldn = absx(dot3(-l, ln));
+  if (ndl > 0.0f && ldn > 0.0f) {
+    v3 so = hit_pos + n_geo * 0.001f;
+    float vis = trace_shadow<STATS>(c, so, lp, p.seed, cnt);
+    vis = fmaxx(vis, transmission);
+    if (vis > 0.0f) {
+      const ptgs_material& lm = sc.materials[tri.material_index];
+      v3 le = ld3(lm.emissive_factor_and_pad);
+      float es = fmaxx(le.x, fmaxx(le.y, le.z));
+      float pdf_nee = (es / c.cp->emissive_flux) * (dist_sq / ldn);
+      float prob_spec;
+      float pdf_spec, pdf_diff;
+      if (sg) {
+        pdf_spec = pdf_ggx(n, v, l, roughness);
+        pdf_diff = pdf_lambert(n, l);
+        prob_spec = clampf(length3(f0), 0.05f, 0.95f);
+      } else {
+        prob_spec = mixf(0.04f, 1.0f, metallic);
+        pdf_spec = pdf_ggx(n, v, l, roughness);
+        pdf_diff = pdf_lambert(n, l);
+      }
+      float prob_diff = 1.0f - prob_spec;
+      float pdf_bsdf = pdf_spec * prob_spec + pdf_diff * prob_diff;
+      float mis = (pdf_nee * pdf_nee) / (pdf_nee * pdf_nee + pdf_bsdf * pdf_bsdf);
+      v3 h = safe_normalize(v + l);
+      float ndf = d_ggx(n, h, roughness);
+      float vis_t = v_smith(dot3(n, v), ndl, roughness);
+      v3 f = f_schlick(dot3(h, v), f0);
+      v3 kd = mk3(1.0f) - f;
+      v3 spec = f * (ndf * vis_t);
+      v3 diff = ((kd * albedo) / PT_PI) * (1.0f - transmission);
+      v3 brdf = diff + spec;
+      if (pdf_nee > 1e-10f)
+        lo = lo + (((((brdf * le) * ndl) * (1.0f / pdf_nee)) * mis) * vis) * c.cp->ambient[3];
+    }
+  }
+}
+
+
+}  // namespace ptgs

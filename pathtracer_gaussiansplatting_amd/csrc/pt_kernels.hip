@@ -1,0 +1,264 @@
+// pt_kernels.hip — path-tracer kernels for gfx950 (MI355X).
+//
+//   pt_camera_kernel : shaders/rt_render/raygen_camera.rgen:17-88 (one work-item per pixel,
+//                      `spp` consecutive samples per launch; the running mean of :80-87 is kept in
+//                      registers across samples, which is bit-identical to one RMW per frame).
+//   pt_torus_kernel  : shaders/rt_datacollect/raygen.rgen:31-141 (one work-item per RaySample).
+//
+// Launch geometry: 256-thread workgroups = 4 waves, each wave an 8x8 pixel tile (primary-ray
+// coherence for the BVH walk), workgroup = 16x16 pixels; 1080p -> 8,160 workgroups (>> 256 CUs).
+#include <hip/hip_runtime.h>
+
+#include "pt_shade.h"
+#include "pt_launch.h"
+
+namespace ptgs {
+
+__device__ __forceinline__ v4 matvec(const float* m, v4 v) {
+  // GLSL mat4 * vec4 with columns m[0..3], m[4..7], ...: ((c0*x + c1*y) + c2*z) + c3*w
+  return mk4(((m[0] * v.x + m[4] * v.y) + m[8] * v.z) + m[12] * v.w,
+             ((m[1] * v.x + m[5] * v.y) + m[9] * v.z) + m[13] * v.w,
+             ((m[2] * v.x + m[6] * v.y) + m[10] * v.z) + m[14] * v.w,
+             ((m[3] * v.x + m[7] * v.y) + m[11] * v.z) + m[15] * v.w);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
+  unsigned long long x = v;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+__device__ __forceinline__ void flush_counters(unsigned long long* counters, uint32_t ext, uint32_t shadow,
+                                               uint32_t samples, const TraversalCounters& tc, bool stats) {
+  unsigned long long a = wave_sum(ext), b = wave_sum(shadow), c = wave_sum(samples);
+  unsigned long long d = 0, e = 0;
+  if (stats) { d = wave_sum(tc.nodes); e = wave_sum(tc.tris); }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(counters + 0, a);
+    atomicAdd(counters + 1, b);
+    atomicAdd(counters + 2, c);
+    if (stats) { atomicAdd(counters + 3, d); atomicAdd(counters + 4, e); }
+  }
+}
+
+// r2 offset of the blue-noise lookup (raygen_camera.rgen:11-15, :19-23)
+__device__ __forceinline__ float4 blue_noise_texel(const DevScene& sc, uint32_t lx, uint32_t ly, uint32_t frame) {
+  const float a1 = 0.75487766624669276f;
+  const float a2 = 0.56984029099805327f;
+  float rx = fractx((float)frame * a1);
+  float ry = fractx((float)frame * a2);
+  int ox = (int)(rx * (float)sc.bn_size);
+  int oy = (int)(ry * (float)sc.bn_size);
+  int px = ((int)lx + ox) & (sc.bn_size - 1);
+  int py = ((int)ly + oy) & (sc.bn_size - 1);
+  return sc.blue_noise[py * sc.bn_size + px];
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void pt_camera_kernel(DevScene sc, CamParams cp, float4* __restrict__ accum,
+                                                        uint32_t W, uint32_t H, uint32_t row0, uint32_t row1,
+                                                        uint32_t spp, uint32_t frame0, uint32_t stride,
+                                                        uint32_t mode, unsigned long long* counters) {
+  const uint32_t lid = threadIdx.x;
+  const uint32_t wave = lid >> 6, lane = lid & 63u;
+  const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+  const uint32_t y = row0 + blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+  const bool active = (x < W) && (y < row1);
+
+  ShadeCtx c; c.sc = &sc; c.cp = &cp; c.shadow_rays = 0;
+  TraversalCounters tc; tc.nodes = 0; tc.tris = 0;
+  uint32_t ext_rays = 0, samples = 0;
+
+  if (active) {
+    const size_t pix = (size_t)y * W + x;
+    v3 state = mk3(0.0f);
+    float state_a = 0.0f;
+    if (mode == PTGS_ACCUM_SUM || frame0 > 0) {
+      float4 prev = accum[pix];
+      state = mk3(prev.x, prev.y, prev.z);
+      state_a = prev.w;
+    }
+    for (uint32_t s = 0; s < spp; ++s) {
+      const uint32_t frame = frame0 + s * stride;
+      float4 blue = blue_noise_texel(sc, x, y, frame);
+      uint32_t index = y * W + x;
+      uint32_t seed = index + frame * 719393u;
+      float pcx = (float)x + blue.x, pcy = (float)y + blue.y;
+      float ux = pcx / (float)W, uy = pcy / (float)H;
+      float dx = ux * 2.0f - 1.0f, dy = uy * 2.0f - 1.0f;
+      v4 origin = matvec(cp.inv_view, mk4(0.f, 0.f, 0.f, 1.f));
+      v4 target = matvec(cp.inv_proj, mk4(dx, dy, 1.f, 1.f));
+      v3 dirc = normalize3(mk3(target.x, target.y, target.z) / target.w);
+      v4 direction = matvec(cp.inv_view, mk4(dirc.x, dirc.y, dirc.z, 0.f));
+      v3 ro = mk3(origin.x, origin.y, origin.z);
+      v3 rd = normalize3(mk3(direction.x, direction.y, direction.z));
+
+      v3 acc = mk3(0.0f);
+      v3 thr = mk3(1.0f);
+      Payload p;
+      p.seed = seed;
+      p.blue = mk2(blue.z, blue.w);
+      p.last_pdf = 0.0f;
+      p.hit_flag = 0.0f;
+      p.color = mk3(0.0f); p.weight = mk3(1.0f); p.next_o = ro; p.next_d = rd;
+      int max_depth = 12;
+      for (int depth = 0; depth < max_depth; ++depth) {
+        p.depth = depth;
+        Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
+        ext_rays++;
+        Hit h = trace_closest<STATS>(sc, ray, p.seed, tc);
+        if (h.gid == 0xffffffffu) miss<false>(cp, p);
+        else closest_hit<STATS, false>(c, p, ray, h, tc);
+        acc = acc + p.color * thr;
+        acc = vmin(acc, 5.0f);
+        if (p.hit_flag < 0.0f) break;
+        if (depth == 0 && p.hit_flag < 1.5f) max_depth = 4;
+        thr = thr * p.weight;
+        ro = p.next_o;
+        rd = p.next_d;
+        float mt = fmaxx(fmaxx(thr.x, thr.y), thr.z);
+        if (mt < 0.001f) break;
+        if (depth >= 4) {
+          float pr = clampf(mt, 0.05f, 0.95f);
+          if (rnd(p.seed) > pr) break;
+          thr = thr / pr;
+        }
+      }
+      if (mode == PTGS_ACCUM_SUM) {
+        state = state + acc;
+        state_a = state_a + 1.0f;
+      } else if (frame > 0) {
+        float blend = 1.0f / (float)(frame + 1u);
+        state = mix3(state, acc, blend);
+      } else {
+        state = acc;
+      }
+      samples++;
+    }
+    if (mode == PTGS_ACCUM_SUM) accum[pix] = make_float4(state.x, state.y, state.z, state_a);
+    else accum[pix] = make_float4(state.x, state.y, state.z, 1.0f);
+  }
+  flush_counters(counters, ext_rays, c.shadow_rays, samples, tc, STATS);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp, TorusParams tp,
+                                                       const ptgs_ray_sample* __restrict__ samples,
+                                                       uint32_t n, uint32_t side, uint32_t frame,
+                                                       ptgs_hitdata* __restrict__ hits,
+                                                       unsigned long long* counters) {
+  const uint32_t index = blockIdx.x * blockDim.x + threadIdx.x;
+  ShadeCtx c; c.sc = &sc; c.cp = &cp; c.shadow_rays = 0;
+  TraversalCounters tc; tc.nodes = 0; tc.tris = 0;
+  uint32_t ext_rays = 0, nsamp = 0;
+  if (index < n) {
+    const uint32_t lx = index % side, ly = index / side;
+    uint32_t light_seed = index + frame * 719393u;
+    ptgs_ray_sample smp = samples[index];
+    float u = (smp.uv[0] * 2.0f) * PT_PI;
+    float v = (smp.uv[1] * 2.0f) * PT_PI;
+    float R = tp.major_radius, r = tp.minor_radius, hh = tp.height;
+    float su, cu, sv, cv;
+    sincosx(u, &su, &cu);
+    sincosx(v, &sv, &cv);
+    v3 lp = mk3((R + r * cv) * cu, r * sv + hh, (R + r * cv) * su);
+    v3 ln = mk3(cv * cu, sv, cv * su);
+    v4 wo = matvec(tp.model, mk4(lp.x, lp.y, lp.z, 1.0f));
+    v4 wn4 = matvec(tp.model, mk4(ln.x, ln.y, ln.z, 0.0f));
+    v3 wn = normalize3(mk3(wn4.x, wn4.y, wn4.z));
+    v3 rd = wn;
+    v3 so = mk3(wo.x, wo.y, wo.z) + rd * 0.05f;
+
+    float4 blue = blue_noise_texel(sc, lx, ly, frame);
+    v3 acc = mk3(0.0f);
+    v3 thr = mk3(1.0f);
+    Payload p;
+    p.seed = light_seed;
+    p.last_pdf = 0.0f;
+    p.blue = mk2(blue.z, blue.w);
+    p.depth = 0;
+    p.hit_flag = 0.0f;
+    p.color = mk3(0.0f); p.weight = mk3(1.0f); p.next_o = so; p.next_d = rd;
+    p.hit_pos = mk3(0.0f); p.normal = mk3(0.0f, 1.0f, 0.0f);
+
+    Ray ray = make_ray(so, rd, 0.0f, 10000.0f);
+    ext_rays++;
+    Hit h = trace_closest<STATS>(sc, ray, p.seed, tc);
+    if (h.gid == 0xffffffffu) miss<true>(cp, p);
+    else closest_hit<STATS, true>(c, p, ray, h, tc);
+
+    v3 fpos = p.hit_pos;
+    float fflag = p.hit_flag;
+    v3 fnorm = p.normal;
+    if (p.hit_flag > 0.5f) {
+      acc = acc + p.color * thr;
+      for (int depth = 1; depth < 12; ++depth) {
+        p.depth = depth;
+        thr = thr * p.weight;
+        float mt = fmaxx(fmaxx(thr.x, thr.y), thr.z);
+        if (mt < 0.001f) break;
+        if (depth >= 4) {
+          float pr = clampf(mt, 0.05f, 0.95f);
+          if (rnd(p.seed) > pr) break;
+          thr = thr / pr;
+        }
+        Ray r2 = make_ray(p.next_o, p.next_d, 0.001f, 10000.0f);
+        ext_rays++;
+        Hit h2 = trace_closest<STATS>(sc, r2, p.seed, tc);
+        if (h2.gid == 0xffffffffu) miss<true>(cp, p);
+        else closest_hit<STATS, true>(c, p, r2, h2, tc);
+        acc = acc + p.color * thr;
+        acc = vmin(acc, 5.0f);
+        if (p.hit_flag < 1.5f) break;
+      }
+    }
+    v3 cur = acc;
+    ptgs_hitdata hd = hits[index];
+    if (frame > 0) {
+      v3 prev = mk3(hd.color[0], hd.color[1], hd.color[2]);
+      float bf = 1.0f / (float)(frame + 1u);
+      cur = mix3(prev, cur, bf);
+    }
+    hd.pos[0] = fpos.x; hd.pos[1] = fpos.y; hd.pos[2] = fpos.z;
+    hd.flag = fflag;
+    hd.normal[0] = fnorm.x; hd.normal[1] = fnorm.y; hd.normal[2] = fnorm.z;
+    hd.color[0] = cur.x; hd.color[1] = cur.y; hd.color[2] = cur.z; hd.color[3] = 1.0f;
+    hits[index] = hd;
+    nsamp = 1;
+  }
+  flush_counters(counters, ext_rays, c.shadow_rays, nsamp, tc, STATS);
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accum, uint32_t W, uint32_t H,
+                            uint32_t row0, uint32_t row1, uint32_t spp, uint32_t frame0, uint32_t stride,
+                            uint32_t mode, unsigned long long* counters, bool stats, hipStream_t stream) {
+  if (row1 <= row0 || spp == 0) return hipSuccess;
+  dim3 grid((W + 15u) / 16u, (row1 - row0 + 15u) / 16u);
+  dim3 block(256);
+  if (stats)
+    hipLaunchKernelGGL(pt_camera_kernel<true>, grid, block, 0, stream, sc, cp, (float4*)accum, W, H, row0, row1,
+                       spp, frame0, stride, mode, counters);
+  else
+    hipLaunchKernelGGL(pt_camera_kernel<false>, grid, block, 0, stream, sc, cp, (float4*)accum, W, H, row0, row1,
+                       spp, frame0, stride, mode, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_pt_torus(const DevScene& sc, const CamParams& cp, const TorusParams& tp,
+                           const ptgs_ray_sample* samples, uint32_t n, uint32_t side, uint32_t frame,
+                           ptgs_hitdata* hits, unsigned long long* counters, bool stats, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  dim3 grid((n + 255u) / 256u);
+  dim3 block(256);
+  if (stats)
+    hipLaunchKernelGGL(pt_torus_kernel<true>, grid, block, 0, stream, sc, cp, tp, samples, n, side, frame, hits, counters);
+  else
+    hipLaunchKernelGGL(pt_torus_kernel<false>, grid, block, 0, stream, sc, cp, tp, samples, n, side, frame, hits, counters);
+  return hipGetLastError();
+}
+
+}  // namespace ptgs

@@ -1,0 +1,23 @@
+// pt_launch.h — host-visible launch interface of the path-tracer kernels (pt_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include "pt_device.h"
+
+namespace ptgs {
+
+// RayPushConstant fields read by rt_datacollect/raygen.rgen:13-19
+struct TorusParams {
+  float model[16];
+  float major_radius, minor_radius, height;
+};
+
+hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accum, uint32_t W, uint32_t H,
+                            uint32_t row0, uint32_t row1, uint32_t spp, uint32_t frame0, uint32_t stride,
+                            uint32_t mode, unsigned long long* counters, bool stats, hipStream_t stream);
+
+hipError_t launch_pt_torus(const DevScene& sc, const CamParams& cp, const TorusParams& tp,
+                           const ptgs_ray_sample* samples, uint32_t n, uint32_t side, uint32_t frame,
+                           ptgs_hitdata* hits, unsigned long long* counters, bool stats, hipStream_t stream);
+
+}  // namespace ptgs

@@ -1,0 +1,259 @@
+// pt_shade.h — closest-hit shading, restating shaders/rt_render/closesthit.rchit:324-621
+// (WITH_HITPOS = the rt_datacollect variant, which also writes payload.hit_pos / normal,
+// shaders/rt_datacollect/closesthit.rchit:443-447). Textures are not sampled yet: every
+// sampleTexture() behind an "id > 0" guard returns vec4(1) (untextured scenes are exact; see
+// DESIGN.md "textures").
+#pragma once
+
+#include "pt_device.h"
+
+namespace ptgs {
+
+template <bool STATS, bool WITH_HITPOS>
+__device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& hit, TraversalCounters& cnt) {
+  const DevScene& sc = *c.sc;
+  const CamParams& cp = *c.cp;
+
+  const float4* rec = sc.tris + 3u * hit.slot;
+  uint32_t mesh = f2u(rec[0].w);
+  uint32_t prim = f2u(rec[1].w);
+  const ptgs_mesh_info info = sc.meshes[mesh];
+  const ptgs_material& mat = sc.materials[info.material_index];
+
+  uint32_t i0 = sc.indices[info.index_offset + prim * 3u + 0u];
+  uint32_t i1 = sc.indices[info.index_offset + prim * 3u + 1u];
+  uint32_t i2 = sc.indices[info.index_offset + prim * 3u + 2u];
+  const ptgs_vertex& v0 = sc.vertices[info.vertex_offset + i0];
+  const ptgs_vertex& v1 = sc.vertices[info.vertex_offset + i1];
+  const ptgs_vertex& v2 = sc.vertices[info.vertex_offset + i2];
+
+  // :336-346
+  float bx = (1.0f - hit.u) - hit.v, by = hit.u, bz = hit.v;
+  v3 hit_pos = ray.o + ray.d * hit.t;
+  v3 vcol = (ld3(v0.color) * bx + ld3(v1.color) * by) + ld3(v2.color) * bz;
+  v3 nobj = (ld3(v0.normal) * bx + ld3(v1.normal) * by) + ld3(v2.normal) * bz;
+  v3 tobj = (ld3(v0.tangent) * bx + ld3(v1.tangent) * by) + ld3(v2.tangent) * bz;
+  float tw = (v0.tangent[3] * bx + v1.tangent[3] * by) + v2.tangent[3] * bz;
+  // instance transforms are identity (transforms are baked into vertices, engine.cpp:1294-1338)
+  v3 n_geo = safe_normalize(nobj);
+  v3 t_geo = safe_normalize(tobj);
+  t_geo = safe_normalize(t_geo - n_geo * dot3(t_geo, n_geo));
+  (void)t_geo;
+
+  v3 V = -ray.d;
+  v3 n_geo_orig = n_geo;
+  if (dot3(n_geo, V) < 0.0f) n_geo = -n_geo;
+  v3 N = n_geo;
+  v3 T = t_geo;
+  bool tangent_valid = (absx(tw) > 0.001f) && (length3(T) > 0.001f);
+  if (!tangent_valid) {
+    v3 up = (absx(N.y) < 0.999f) ? mk3(0.f, 1.f, 0.f) : mk3(1.f, 0.f, 0.f);
+    T = safe_normalize(cross3(up, N));
+  }
+  // Normal map (:364-385) needs textures, which are not uploaded yet: the block is skipped, so
+  // N stays the flipped geometric normal (exact for scenes without normal_id > 0).
+  (void)T;
+
+  v3 albedo, f0;
+  float roughness, metallic;
+  int32_t sg_bits;
+  {
+    union { float f; int32_t i; } pun; pun.f = mat.use_specular_glossiness_workflow;
+    sg_bits = pun.i;  // float stored, int read
+  }
+  v3 bcf = mk3(mat.base_color_factor[0], mat.base_color_factor[1], mat.base_color_factor[2]);
+  if ((float)sg_bits > 0.5f) {
+    albedo = bcf * vcol;  // * base_color_sample (1)
+    v3 spec_col = ld3(mat.specular_color_factor);
+    float gloss = mat.roughness_factor;
+    f0 = spec_col;
+    roughness = sqrtx(fmaxx(1.0f - gloss, 0.04f));
+    metallic = 0.0f;
+  } else {
+    albedo = bcf * vcol;
+    metallic = mat.metallic_factor;
+    roughness = mat.roughness_factor;
+    f0 = mix3(mk3(0.04f), albedo, metallic);
+    albedo = albedo * (1.0f - metallic);
+  }
+  float clearcoat = mat.clearcoat_factor;
+  float cc_rough = mat.clearcoat_roughness_factor;
+  v3 emissive = ld3(mat.emissive_factor_and_pad);
+  float transmission = mat.transmission_factor;
+
+  if (WITH_HITPOS) {
+    p.hit_pos = hit_pos;
+    p.normal = N;
+  }
+
+  // :444-468
+  v3 lo = mk3(0.0f);
+  v3 le = emissive;
+  float es = length3(emissive);
+  bool use_nee = (transmission == 0.0f) && (roughness > 0.001f);
+  if (p.hit_flag > 3.0f) use_nee = false;
+  if (es > 0.0f) {
+    if (p.last_pdf <= 0.0f || !use_nee) {
+      lo = lo + le;
+    } else if (es < 0.001f) {
+      p.color = mk3(0.0f);
+      return;
+    } else {
+      float pdf_bsdf = p.last_pdf;
+      float es_cpu = length3(ld3(mat.emissive_factor_and_pad));
+      v3 l_to_cam = -ray.d;
+      float ldn = absx(dot3(N, l_to_cam));
+      float dist_sq = hit.t * hit.t;
+      float pdf_nee = 0.0f;
+      if (cp.emissive_flux > 0.0f) pdf_nee = (es_cpu / cp.emissive_flux) * (dist_sq / fmaxx(ldn, 0.001f));
+      float prob_nee = (cp.punctual_flux > 0.0f) ? cp.p_emissive : 1.0f;
+      pdf_nee = pdf_nee * prob_nee;
+      float mis = (pdf_bsdf * pdf_bsdf) / (pdf_bsdf * pdf_bsdf + pdf_nee * pdf_nee);
+      lo = lo + le * mis;
+    }
+  }
+
+  // :470-494
+  bool has_emissive = cp.emissive_flux > 0.0f;
+  bool has_punctual = cp.punctual_flux > 0.0f;
+  bool sg = (float)sg_bits > 0.0f;
+  if (has_emissive && has_punctual) {
+    v3 lc = mk3(0.0f);
+    float p_punctual = 1.0f - cp.p_emissive;
+    if (blue_noise_dim(p, 10) < cp.p_emissive) {
+      if (use_nee) {
+        sample_emissive<STATS>(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, lc, cnt);
+        lc = lc * (1.0f / cp.p_emissive);
+      }
+    } else {
+      sample_punctual<STATS>(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, lc, cnt);
+      lc = lc * (1.0f / p_punctual);
+    }
+    lo = lo + lc;
+  } else if (has_emissive && use_nee) {
+    sample_emissive<STATS>(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, lo, cnt);
+  } else if (has_punctual) {
+    sample_punctual<STATS>(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, lo, cnt);
+  }
+  p.color = lo;
+
+  // :503-531 glass
+  if (transmission > 0.0f) {
+    p.hit_flag = 2.0f;
+    bool entering = dot3(n_geo_orig, V) > 0.0f;
+    v3 n_refr = entering ? n_geo_orig : -n_geo_orig;
+    p.next_o = hit_pos - n_refr * 0.001f;
+    v3 fv = f_schlick(absx(dot3(n_geo_orig, V)), f0);
+    float prob_reflect = fmaxx(fmaxx(fv.x, fv.y), fv.z);
+    if (blue_noise_dim(p, 11) < prob_reflect) {
+      p.next_o = hit_pos + n_refr * 0.001f;
+      p.next_d = reflect3(-V, n_refr);
+      p.weight = mk3(1.0f);
+    } else {
+      const float ior = 1.01f;
+      float eta = entering ? (1.0f / ior) : ior;
+      v3 rd = refract3(-V, n_refr, eta);
+      if (length3(rd) > 0.0f) {
+        p.next_d = rd;
+        p.weight = albedo;
+      } else {
+        p.next_o = hit_pos + n_geo * 0.001f;
+        p.next_d = reflect3(-V, N);
+        p.weight = mk3(1.0f);
+      }
+    }
+    p.last_pdf = 0.0f;
+    return;
+  }
+
+  // :534-620 opaque
+  p.hit_flag = 1.0f;
+  p.next_o = hit_pos + n_geo * 0.001f;
+  float ndv = fmaxx(dot3(N, V), 0.0f);
+  float cc_prob = 0.0f;
+  v3 f_cc_view = mk3(0.0f);
+  if (clearcoat > 0.0f) {
+    f_cc_view = f_schlick(ndv, mk3(0.04f)) * clearcoat;
+    cc_prob = clampf(fmaxx(f_cc_view.x, fmaxx(f_cc_view.y, f_cc_view.z)), 0.0f, 1.0f);
+  }
+  if (clearcoat > 0.0f && blue_noise_dim(p, 12) < cc_prob) {
+    v3 hcc = sample_ggx(p, N, cc_rough);
+    v3 lcc = reflect3(-V, hcc);
+    float ndl = fmaxx(dot3(N, lcc), 0.0f);
+    float ndh = fmaxx(dot3(N, hcc), 0.0f);
+    float vdh = fmaxx(dot3(V, hcc), 0.0f);
+    if (dot3(lcc, n_geo) <= 0.0f) {
+      p.weight = mk3(0.0f);
+      p.last_pdf = 0.0f;
+    } else {
+      p.next_d = lcc;
+      v3 f = f_schlick(vdh, mk3(0.04f)) * clearcoat;
+      float vis = v_smith(ndv, ndl, cc_rough);
+      v3 sw = ((f * vis) * 4.0f) * ndl * (vdh / fmaxx(ndh, 0.0001f));
+      float pdf_cc = pdf_ggx(N, V, lcc, cc_rough);
+      float psb = mixf(0.04f, 1.0f, metallic);
+      psb = mixf(psb, 1.0f, pow5(1.0f - ndv));
+      psb = clampf(psb, 0.05f, 0.95f);
+      float pdb = 1.0f - psb;
+      float pdf_sb = pdf_ggx(N, V, lcc, roughness);
+      float pdf_db = pdf_lambert(N, lcc);
+      float pdf_base = pdf_sb * psb + pdf_db * pdb;
+      p.last_pdf = pdf_cc * cc_prob + pdf_base * (1.0f - cc_prob);
+      p.weight = sw * (1.0f / cc_prob);
+    }
+  } else {
+    v3 tf = mk3(1.0f) - f_cc_view;
+    float selw = 1.0f / (1.0f - cc_prob);
+    v3 ea = tf * selw;
+    float ps = mixf(0.04f, 1.0f, metallic);
+    ps = mixf(ps, 1.0f, pow5(1.0f - ndv));
+    ps = clampf(ps, 0.05f, 0.95f);
+    float pd = 1.0f - ps;
+    if (blue_noise_dim(p, 13) < ps) {
+      v3 h = sample_ggx(p, N, roughness);
+      v3 l = reflect3(-V, h);
+      float ndl = fmaxx(dot3(N, l), 0.0f);
+      float ndh = fmaxx(dot3(N, h), 0.0f);
+      float vdh = fmaxx(dot3(V, h), 0.0f);
+      if (dot3(l, n_geo) <= 0.0f) {
+        p.weight = mk3(0.0f);
+        p.last_pdf = 0.0f;
+      } else {
+        p.next_d = l;
+        v3 f = f_schlick(fmaxx(dot3(h, V), 0.0f), f0);
+        float vis = v_smith(ndv, ndl, roughness);
+        v3 sw = ((f * vis) * 4.0f) * ndl * (vdh / fmaxx(ndh, 0.0001f));
+        float pdf_s = pdf_ggx(N, V, l, roughness);
+        float pdf_d = pdf_lambert(N, l);
+        p.last_pdf = (pdf_s * ps + pdf_d * pd) * (1.0f - cc_prob);
+        p.weight = (sw * (1.0f / ps)) * ea;
+      }
+    } else {
+      v3 l = sample_cosine(p, N);
+      if (dot3(l, n_geo) <= 0.0f) {
+        p.weight = mk3(0.0f);
+        p.last_pdf = 0.0f;
+      } else {
+        p.next_d = l;
+        p.weight = (albedo * (1.0f / (1.0f - ps))) * ea;
+        float pdf_s = pdf_ggx(N, V, l, roughness);
+        float pdf_d = pdf_lambert(N, l);
+        p.last_pdf = (pdf_s * ps + pdf_d * pd) * (1.0f - cc_prob);
+      }
+    }
+  }
+}
+
+// miss.rmiss:9-14 (rt_datacollect/miss.rmiss also resets hit_pos / normal)
+template <bool WITH_HITPOS>
+__device__ __forceinline__ void miss(const CamParams& cp, Payload& p) {
+  p.hit_flag = -1.0f;
+  p.color = mk3(cp.ambient[0], cp.ambient[1], cp.ambient[2]) * 2.0f;
+  p.weight = mk3(1.0f);
+  if (WITH_HITPOS) {
+    p.hit_pos = mk3(0.0f);
+    p.normal = mk3(0.0f, 1.0f, 0.0f);
+  }
+}
+
+}  // namespace ptgs

@@ -1,0 +1,30 @@
+// splat.h — Gaussian-splatting / point-splat workspace owned by a ptgs_ctx (see splat.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ptgs/ptgs.h"
+
+namespace ptgs {
+
+struct SplatWorkspace;
+SplatWorkspace* splat_workspace_create();
+void splat_workspace_destroy(SplatWorkspace* w);
+
+// view/mvp column-major float[16]; p00 = proj[0][0], p11 = proj[1][1] (negative: Vulkan y-down)
+hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
+                           float p11, uint32_t W, uint32_t H, const float bg[3], uint32_t tile_row_begin,
+                           uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, hipStream_t s);
+void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out);
+hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long** keys);
+
+// GLSL mat4 * mat4, column-major, fixed evaluation order ((a0*b0 + a1*b1) + a2*b2) + a3*b3
+inline void mat4_mul(const float* a, const float* b, float* out) {
+  for (int c = 0; c < 4; ++c)
+    for (int r = 0; r < 4; ++r)
+      out[c * 4 + r] = ((a[0 * 4 + r] * b[c * 4 + 0] + a[1 * 4 + r] * b[c * 4 + 1]) + a[2 * 4 + r] * b[c * 4 + 2]) +
+                       a[3 * 4 + r] * b[c * 4 + 3];
+}
+
+}  // namespace ptgs

@@ -1,0 +1,161 @@
+"""Renderer: the device-side API over libptgs.so (the drop-in for the reference's RT pipeline).
+
+Mirrors what Engine does around the hot path (Vulkan_Engine/engine.cpp):
+  upload_scene(scene)              createGlobalBindlessBuffers + buildBlas/initStaticTlas
+  trace_camera(ubo, accum, spp)    vkCmdTraceRaysKHR(W,H,1) x spp + running mean (:1971, :2684-2708)
+  trace_torus(...)                 torus trace (:1893-1900, :2787-2794)
+  splat_points(...)                point-cloud draw (:1945-1961)
+  splat_gaussians(...)             3DGS forward (absent from the reference)
+  encode_srgb8(...)                rgba32f -> sRGB8 blit (:2004-2020)
+Device buffers are torch tensors on the context's device (or raw device pointers as ints).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import Gaussians, RayPush, SceneInfo, SplatBuffers, SplatStats, TraceStats, Ubo
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        if not x.is_cuda:
+            raise _abi.PtgsError("expected a device tensor (got a host tensor): the renderer has no CPU path")
+        if not x.is_contiguous():
+            raise _abi.PtgsError("device tensor must be contiguous")
+        return x.data_ptr()
+    raise TypeError(f"cannot take a device pointer of {type(x)}")
+
+
+def _stream(stream) -> int:
+    if stream is None:
+        try:
+            import torch
+            return torch.cuda.current_stream().cuda_stream
+        except Exception:
+            return 0
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+class Renderer:
+    def __init__(self, device: int = 0):
+        self.lib = _abi.load_library()
+        h = C.c_void_p()
+        rc = self.lib.ptgs_create(int(device), C.byref(h))
+        _abi.check(rc, f"ptgs_create(device={device})")
+        self._h = h
+        self.device = device
+        self.scene = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.ptgs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self) -> str:
+        return (self.lib.ptgs_last_error(self._h) or b"").decode()
+
+    def _chk(self, rc: int, what: str):
+        _abi.check(rc, what, self._err())
+
+    # ---------------------------------------------------------------- scene
+    def upload_scene(self, scene) -> SceneInfo:
+        d = scene.desc()
+        self._chk(self.lib.ptgs_scene_upload(self._h, C.byref(d)), "ptgs_scene_upload")
+        self.scene = scene
+        return self.scene_info()
+
+    def scene_info(self) -> SceneInfo:
+        info = SceneInfo()
+        self._chk(self.lib.ptgs_scene_get_info(self._h, C.byref(info)), "ptgs_scene_get_info")
+        return info
+
+    # ---------------------------------------------------------------- path tracer
+    def trace_camera(self, ubo: Ubo, width: int, height: int, accum, spp: int = 1, frame_stride: int = 1,
+                     mode: int = _abi.ACCUM_RUNNING_MEAN, rows: tuple | None = None, stream=None):
+        if rows is None:
+            rc = self.lib.ptgs_trace_camera(self._h, C.byref(ubo), width, height, _ptr(accum), spp, frame_stride,
+                                            mode, _stream(stream))
+        else:
+            rc = self.lib.ptgs_trace_camera_rows(self._h, C.byref(ubo), width, height, rows[0], rows[1],
+                                                 _ptr(accum), spp, frame_stride, mode, _stream(stream))
+        self._chk(rc, "ptgs_trace_camera")
+
+    def trace_torus(self, ubo: Ubo, push: RayPush, samples, n: int, hits, stream=None):
+        rc = self.lib.ptgs_trace_torus(self._h, C.byref(ubo), C.byref(push), _ptr(samples), n, _ptr(hits),
+                                       _stream(stream))
+        self._chk(rc, "ptgs_trace_torus")
+
+    def set_flags(self, flags: int):
+        self._chk(self.lib.ptgs_set_flags(self._h, flags), "ptgs_set_flags")
+
+    def stats_reset(self, stream=None):
+        self._chk(self.lib.ptgs_stats_reset(self._h, _stream(stream)), "ptgs_stats_reset")
+
+    def stats(self) -> TraceStats:
+        s = TraceStats()
+        self._chk(self.lib.ptgs_stats_read(self._h, C.byref(s)), "ptgs_stats_read")
+        return s
+
+    # ---------------------------------------------------------------- rasterizers
+    def splat_points(self, ubo: Ubo, push: RayPush, hits, samples, n: int, width: int, height: int, rgba8, depth,
+                     stream=None):
+        rc = self.lib.ptgs_splat_points(self._h, C.byref(ubo), C.byref(push), _ptr(hits), _ptr(samples), n, width,
+                                        height, _ptr(rgba8), _ptr(depth), _stream(stream))
+        self._chk(rc, "ptgs_splat_points")
+
+    def splat_gaussians(self, g: dict, ubo: Ubo, width: int, height: int, out, bg=(0.0, 0.0, 0.0),
+                        tile_rows: tuple | None = None, want_stats: bool = False, stream=None):
+        gs = Gaussians()
+        gs.means, gs.scales, gs.rotations = _ptr(g["means"]), _ptr(g["scales"]), _ptr(g["rotations"])
+        gs.opacities, gs.colors = _ptr(g["opacities"]), _ptr(g["colors"])
+        gs.count = int(g["means"].shape[0])
+        bgc = np.asarray(bg, np.float32)
+        t0, t1 = (0, 0xFFFFFFFF) if tile_rows is None else tile_rows
+        st = SplatStats()
+        rc = self.lib.ptgs_splat_gaussians(self._h, C.byref(gs), C.byref(ubo), width, height, _abi.fptr(bgc), t0,
+                                           t1, _ptr(out), C.byref(st) if want_stats else None, _stream(stream))
+        self._chk(rc, "ptgs_splat_gaussians")
+        return st if want_stats else None
+
+    def splat_buffers(self) -> SplatBuffers:
+        b = SplatBuffers()
+        self._chk(self.lib.ptgs_splat_get_buffers(self._h, C.byref(b)), "ptgs_splat_get_buffers")
+        return b
+
+    def encode_srgb8(self, rgba32f, width: int, height: int, rgba8, stream=None):
+        rc = self.lib.ptgs_encode_srgb8(self._h, _ptr(rgba32f), width, height, _ptr(rgba8), _stream(stream))
+        self._chk(rc, "ptgs_encode_srgb8")
+
+    # ---------------------------------------------------------------- memory helpers
+    def copy_d2h(self, dst: np.ndarray, src_ptr: int, nbytes: int):
+        self._chk(self.lib.ptgs_memcpy_d2h(self._h, dst.ctypes.data, src_ptr, nbytes), "ptgs_memcpy_d2h")
+
+    def synchronize(self):
+        self._chk(self.lib.ptgs_synchronize(self._h), "ptgs_synchronize")
+
+
+def torus_push(model=None, major_radius: float = 3.5, minor_radius: float = 1.0, height: float = 3.0,
+               mode: int = 0) -> RayPush:
+    p = RayPush()
+    m = np.eye(4, dtype=np.float32).reshape(16) if model is None else np.asarray(model, np.float32).reshape(16)
+    p.model[:] = [float(x) for x in m]
+    p.mode = mode
+    p.major_radius = major_radius
+    p.minor_radius = minor_radius
+    p.height = height
+    return p
