@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""Benchmark of the two hot paths on MI355X (contract: one JSON line on rank 0).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Primary metric (BASELINE.json): Mrays/s of the path tracer on C3 — the 250k-triangle Sponza-like
+atrium at 1920x1080, 64 samples per pixel per GPU (one step = one 64-spp frame = one launch of
+pt_camera_kernel). Rays = extension + shadow segments, counted exactly by the kernel.
+Multi-GPU: sample-index shard (rank g renders frame counts g, g+N, ...; weak scaling: 64 spp per
+GPU) + one RCCL reduce (sum) of the radiance buffer to rank 0 inside the timed region.
+Secondary (same JSON line, "gs"): 3DGS forward on C2 — 100k Gaussians at 1920x1080, Gsplats/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/s (path trace) + Gsplats/s (3DGS) at 1920×1080, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--triangles", type=int, default=250_000)
+    ap.add_argument("--gaussians", type=int, default=100_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gs", action="store_true")
+    ap.add_argument("--no-pt", action="store_true")
+    ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented counting pass")
+    return ap.parse_args()
+
+
+def log2ceil(n):
+    return max(0, math.ceil(math.log2(max(n, 1))))
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    from pathtracer_gaussiansplatting_amd import (ACCUM_RUNNING_MEAN, ACCUM_SUM, FLAG_COUNT_TRAVERSAL,
+                                                  FLAG_TIME_STAGES, Camera, Renderer, make_ubo)
+    from pathtracer_gaussiansplatting_amd import synthetic as Y
+
+    W, H, SPP = args.width, args.height, args.spp
+    r = Renderer(local)
+    stream = torch.cuda.current_stream()
+    out = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32"}
+
+    # ------------------------------------------------------------------ path tracer (C3)
+    if not args.no_pt:
+        scene = Y.atrium_scene(target_tris=args.triangles, seed=2)
+        scene.blue_noise = Y.blue_noise(1024)
+        info = r.upload_scene(scene)
+        pose = Camera(aspect=W / H).look_at([-15.0, 4.0, 5.0], [10.0, 3.0, -3.0])
+        accum = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        mode = ACCUM_RUNNING_MEAN if world == 1 else ACCUM_SUM
+        frame_base = 0
+
+        def pt_step(ev0=None, ev1=None):
+            nonlocal frame_base
+            # sample shard: global sample index s*world + rank (frame_stride = world)
+            ubo = make_ubo(pose, scene, frame_base * world + rank, ambient=(0.3, 0.4, 0.5, 1.0), height=H)
+            if mode == ACCUM_SUM:
+                accum.zero_()
+            if ev0 is not None:
+                ev0.record(stream)
+            r.trace_camera(ubo, W, H, accum, spp=SPP, frame_stride=world, mode=mode, stream=stream)
+            if ev1 is not None:
+                ev1.record(stream)
+            if world > 1:
+                dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)
+            frame_base += SPP
+
+        for _ in range(args.warmup):
+            pt_step()
+        torch.cuda.synchronize()
+        r.stats_reset(stream)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            pt_step(*evs[k])
+        torch.cuda.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        st = r.stats()
+        rays_local = float(st.extension_rays + st.shadow_rays)
+        dt_max = max_over_ranks(dt)
+        rays_total = sum_over_ranks(rays_local)
+        mrays = rays_total / dt_max / 1e6
+        # instrumented counting pass (same scene / camera, count_spp samples) -> bytes per ray
+        r.set_flags(FLAG_COUNT_TRAVERSAL)
+        r.stats_reset(stream)
+        tmp = torch.zeros_like(accum)
+        cnt_ubo = make_ubo(pose, scene, 0, ambient=(0.3, 0.4, 0.5, 1.0), height=H)
+        r.trace_camera(cnt_ubo, W, H, tmp, spp=args.count_spp, mode=ACCUM_RUNNING_MEAN, stream=stream)
+        torch.cuda.synchronize()
+        cs = r.stats()
+        r.set_flags(0)
+        del tmp
+        n_l = len(scene.light_cdf)
+        rays_c = cs.extension_rays + cs.shadow_rays
+        bytes_c = (cs.node_visits * 32 + cs.tri_tests * 36 + cs.closest_hits * 576
+                   + cs.shadow_rays * (16 * log2ceil(n_l) + 16 + 3 * 80 + 308)
+                   + cs.samples * (16 + 16 + 16))
+        bytes_per_ray = bytes_c / max(rays_c, 1)
+        rays_per_launch = rays_local / args.steps
+        alg_bytes = bytes_per_ray * rays_per_launch
+        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
+        if os.path.exists(tpath):
+            try:
+                tj = json.load(open(tpath))
+                e = tj.get("pt_camera_kernel", {})
+                if e.get("workload") == f"C3 {W}x{H} {SPP}spp {args.triangles}tri":
+                    traffic = e.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out.update({
+            "value": round(mrays, 3), "unit": "Mrays/s", "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+            "data": "synthetic: seeded procedural 250k-triangle atrium (no dataset/network)",
+            "config": {"workload": f"C3 path trace: {args.triangles}-tri Sponza-like atrium, {W}x{H}, {SPP} spp per GPU",
+                       "width": W, "height": H, "spp_per_gpu": SPP, "triangles": int(info.num_triangles),
+                       "bvh_nodes": int(info.num_bvh_nodes), "bvh_depth": int(info.bvh_depth),
+                       "parallelism": "single GPU" if world == 1 else f"sample-shard x{world} + RCCL reduce"},
+            "rays_per_step": rays_total / args.steps,
+            "samples_per_s": st.samples * world / dt_max,
+            "kernel_ms": round(kernel_ms, 3),
+            "roofline": {"bound": "hbm", "kernel": "pt_camera_kernel", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                         "bytes_per_ray": round(bytes_per_ray, 2),
+                         "counts_per_ray": {"node_visits": cs.node_visits / max(rays_c, 1),
+                                            "tri_tests": cs.tri_tests / max(rays_c, 1)}},
+        })
+        del accum
+
+    # ------------------------------------------------------------------ 3DGS (C2)
+    if not args.no_gs:
+        g = Y.gaussians_c2(args.gaussians, seed=1 + rank)
+        dg = {k: torch.from_numpy(v).cuda() for k, v in g.items()}
+        gpose = Camera(aspect=W / H).look_at([0.0, 0.0, 0.0], [0.0, 0.0, -1.0])
+        from pathtracer_gaussiansplatting_amd import cornell_box_scene
+        gubo = make_ubo(gpose, cornell_box_scene(), 0)
+        img = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        r.set_flags(FLAG_TIME_STAGES)
+        for _ in range(max(args.warmup, 1)):
+            r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
+        torch.cuda.synchronize()
+        gsteps = max(args.steps, 5)
+        stages = np.zeros(6)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(gsteps):
+            st = r.splat_gaussians(dg, gubo, W, H, img, want_stats=True, stream=stream)
+            stages += r.splat_stage_ms()
+        torch.cuda.synchronize()
+        barrier()
+        gdt = max_over_ranks(time.perf_counter() - t0)
+        r.set_flags(0)
+        stages /= gsteps
+        N = args.gaussians
+        K = st.num_rendered
+        P = math.ceil((32 + log2ceil(st.tiles_x * st.tiles_y)) / 8)
+        b_gs = N * (56 + 48) + N * 48 + K * 12 + P * K * 24 + K * (4 + 48) + W * H * 16
+        gms = gdt / gsteps * 1e3
+        out["gs"] = {
+            "value": round(N * world / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
+            "workload": f"C2 3DGS forward: {N} synthetic Gaussians, {W}x{H}", "pairs_K": int(K),
+            "stages_ms": {k: round(float(v), 4) for k, v in
+                          zip(["preprocess", "scan", "duplicate", "sort", "ranges", "blend"], stages)},
+            "roofline": {"bound": "hbm", "kernel": "whole pipeline", "achieved": round(b_gs / (gms * 1e-3) / 1e9, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(b_gs / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "alg_bytes": b_gs},
+        }
+        if args.no_pt:
+            out.update({"value": out["gs"]["value"], "unit": "Gsplats/s", "ms_per_step": out["gs"]["ms_per_step"],
+                        "config": {"workload": out["gs"]["workload"]}, "data": "synthetic Gaussians (seeded)"})
+
+    # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_pt:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        oracle.build()
+        threads = min(16, os.cpu_count() or 1)
+        row_stride, spp_cpu = 2, 8  # ~10-30 s of CPU work on the box
+        acc = np.zeros((H, W, 4), np.float32)
+        desc = scene.desc()
+        cubo = make_ubo(pose, scene, 0, ambient=(0.3, 0.4, 0.5, 1.0), height=H)
+        t0 = time.perf_counter()
+        cst = oracle.trace_camera(desc, cubo, W, H, acc, spp=spp_cpu, row_stride=row_stride, threads=threads)
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {
+            "value": round((cst.extension_rays + cst.shadow_rays) / cdt / 1e6, 4), "unit": "Mrays/s",
+            "cores": threads, "kind": "port",
+            "sample": f"C3 scene at {W}x{H}, every {row_stride}th row, {spp_cpu} spp "
+                      f"({cst.samples} samples, {cst.extension_rays + cst.shadow_rays} rays, {cdt:.1f} s, "
+                      f"incl. oracle BVH build)",
+        }
+        if not args.no_gs:
+            t0 = time.perf_counter()
+            oracle.splat_gaussians(g, gubo, W, H)
+            gcdt = time.perf_counter() - t0
+            out["cpu_baseline"]["gs"] = {"value": round(args.gaussians / gcdt / 1e9, 6), "unit": "Gsplats/s",
+                                         "cores": 1, "kind": "port", "sample": "full C2 frame"}
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

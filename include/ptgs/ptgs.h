@@ -253,9 +253,11 @@ typedef struct ptgs_trace_stats {
     uint64_t samples;        /* pixel samples completed */
     uint64_t node_visits;    /* child-box tests (only with PTGS_FLAG_COUNT_TRAVERSAL) */
     uint64_t tri_tests;      /* ray-triangle tests (only with PTGS_FLAG_COUNT_TRAVERSAL) */
+    uint64_t closest_hits;   /* extension rays that hit a surface (only with PTGS_FLAG_COUNT_TRAVERSAL) */
 } ptgs_trace_stats;
 
-#define PTGS_FLAG_COUNT_TRAVERSAL 1u
+#define PTGS_FLAG_COUNT_TRAVERSAL 1u /* instrumented kernels: node / triangle / hit counters */
+#define PTGS_FLAG_TIME_STAGES 2u     /* hipEvent timing of the splat pipeline stages */
 int ptgs_set_flags(ptgs_ctx* ctx, uint32_t flags);
 int ptgs_stats_reset(ptgs_ctx* ctx, void* hip_stream);
 int ptgs_stats_read(ptgs_ctx* ctx, ptgs_trace_stats* out); /* synchronises the context's device */
@@ -317,6 +319,11 @@ typedef struct ptgs_splat_buffers {
     uint32_t num_tiles;
 } ptgs_splat_buffers;
 int ptgs_splat_get_buffers(const ptgs_ctx* ctx, ptgs_splat_buffers* out);
+
+/* With PTGS_FLAG_TIME_STAGES: milliseconds of the stages of the most recent ptgs_splat_gaussians
+ * call, measured with hipEvents on its stream: [0] preprocess [1] scan [2] duplicate [3] sort
+ * [4] ranges [5] blend. Synchronises. */
+int ptgs_splat_stage_ms(ptgs_ctx* ctx, float out_ms[6]);
 
 /* ---------------- output encode (blit rgba32f -> B8G8R8A8_SRGB, engine.cpp:2004-2020) --------- */
 /* rgba8 (device W*H u32, R in the low byte): linear -> sRGB8 of clamp(rgb,0,1), alpha 255. */

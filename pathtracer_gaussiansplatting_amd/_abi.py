@@ -19,6 +19,7 @@ ERRORS = {-1: "PTGS_EINVAL", -2: "PTGS_EHIP", -3: "PTGS_ENOSCENE", -4: "PTGS_ERA
 ACCUM_RUNNING_MEAN = 0
 ACCUM_SUM = 1
 FLAG_COUNT_TRAVERSAL = 1
+FLAG_TIME_STAGES = 2
 
 # ---------------------------------------------------------------------------------------------
 # numpy dtypes for the array structs (byte-compatible with Helpers/GeneralHeaders.h)
@@ -97,7 +98,7 @@ class SceneInfo(C.Structure):
 
 class TraceStats(C.Structure):
     _fields_ = [("extension_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("samples", C.c_uint64),
-                ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64)]
+                ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64), ("closest_hits", C.c_uint64)]
 
 
 class Gaussians(C.Structure):
@@ -143,6 +144,7 @@ SYMBOLS = {
     "ptgs_splat_gaussians": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _FP, _U, _U, _P,
                                   C.POINTER(SplatStats), _P]),
     "ptgs_splat_get_buffers": (_I, [_P, C.POINTER(SplatBuffers)]),
+    "ptgs_splat_stage_ms": (_I, [_P, _FP]),
     "ptgs_encode_srgb8": (_I, [_P, _P, _U, _U, _P, _P]),
     "ptgs_device_alloc": (_I, [_P, C.c_size_t, C.POINTER(_P)]),
     "ptgs_device_free": (_I, [_P, _P]),

@@ -304,6 +304,7 @@ int ptgs_stats_read(ptgs_ctx* c, ptgs_trace_stats* out) {
   out->samples = v[2];
   out->node_visits = v[3];
   out->tri_tests = v[4];
+  out->closest_hits = v[5];
   return PTGS_OK;
 }
 
@@ -362,7 +363,8 @@ int ptgs_splat_gaussians(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* u
   float mvp[16];
   mat4_mul(ubo->proj, ubo->view, mvp);
   hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, tile_row_begin,
-                                 tile_row_end, out, stats, (hipStream_t)stream);
+                                 tile_row_end, out, stats, (c->flags & PTGS_FLAG_TIME_STAGES) != 0,
+                                 (hipStream_t)stream);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_gaussians: %s", hipGetErrorString(e));
   return PTGS_OK;
 }
@@ -370,6 +372,13 @@ int ptgs_splat_gaussians(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* u
 int ptgs_splat_get_buffers(const ptgs_ctx* c, ptgs_splat_buffers* out) {
   if (!c || !out) return PTGS_EINVAL;
   splat_get_buffers(c->splat, out);
+  return PTGS_OK;
+}
+
+int ptgs_splat_stage_ms(ptgs_ctx* c, float out_ms[6]) {
+  if (!c || !out_ms) return PTGS_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, splat_stage_ms(c->splat, out_ms));
   return PTGS_OK;
 }
 

@@ -59,8 +59,9 @@ struct Hit {
 };
 
 struct TraversalCounters {
-  uint32_t nodes;
-  uint32_t tris;
+  uint32_t nodes;  // child-box tests
+  uint32_t tris;   // ray-triangle tests
+  uint32_t hits;   // closest hits (shaded surface points)
 };
 
 #define PTGS_STACK 64

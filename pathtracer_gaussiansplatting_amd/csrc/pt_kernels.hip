@@ -32,13 +32,13 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
 __device__ __forceinline__ void flush_counters(unsigned long long* counters, uint32_t ext, uint32_t shadow,
                                                uint32_t samples, const TraversalCounters& tc, bool stats) {
   unsigned long long a = wave_sum(ext), b = wave_sum(shadow), c = wave_sum(samples);
-  unsigned long long d = 0, e = 0;
-  if (stats) { d = wave_sum(tc.nodes); e = wave_sum(tc.tris); }
+  unsigned long long d = 0, e = 0, f = 0;
+  if (stats) { d = wave_sum(tc.nodes); e = wave_sum(tc.tris); f = wave_sum(tc.hits); }
   if ((threadIdx.x & 63) == 0) {
     atomicAdd(counters + 0, a);
     atomicAdd(counters + 1, b);
     atomicAdd(counters + 2, c);
-    if (stats) { atomicAdd(counters + 3, d); atomicAdd(counters + 4, e); }
+    if (stats) { atomicAdd(counters + 3, d); atomicAdd(counters + 4, e); atomicAdd(counters + 5, f); }
   }
 }
 
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void pt_camera_kernel(DevScene sc, CamParams c
   const bool active = (x < W) && (y < row1);
 
   ShadeCtx c; c.sc = &sc; c.cp = &cp; c.shadow_rays = 0;
-  TraversalCounters tc; tc.nodes = 0; tc.tris = 0;
+  TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
   uint32_t ext_rays = 0, samples = 0;
 
   if (active) {
@@ -108,6 +108,7 @@ __global__ __launch_bounds__(256) void pt_camera_kernel(DevScene sc, CamParams c
         Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
         ext_rays++;
         Hit h = trace_closest<STATS>(sc, ray, p.seed, tc);
+        if (STATS && h.gid != 0xffffffffu) tc.hits++;
         if (h.gid == 0xffffffffu) miss<false>(cp, p);
         else closest_hit<STATS, false>(c, p, ray, h, tc);
         acc = acc + p.color * thr;
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
                                                        unsigned long long* counters) {
   const uint32_t index = blockIdx.x * blockDim.x + threadIdx.x;
   ShadeCtx c; c.sc = &sc; c.cp = &cp; c.shadow_rays = 0;
-  TraversalCounters tc; tc.nodes = 0; tc.tris = 0;
+  TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
   uint32_t ext_rays = 0, nsamp = 0;
   if (index < n) {
     const uint32_t lx = index % side, ly = index / side;
@@ -185,6 +186,7 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
     Ray ray = make_ray(so, rd, 0.0f, 10000.0f);
     ext_rays++;
     Hit h = trace_closest<STATS>(sc, ray, p.seed, tc);
+    if (STATS && h.gid != 0xffffffffu) tc.hits++;
     if (h.gid == 0xffffffffu) miss<true>(cp, p);
     else closest_hit<STATS, true>(c, p, ray, h, tc);
 
@@ -206,6 +208,7 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
         Ray r2 = make_ray(p.next_o, p.next_d, 0.001f, 10000.0f);
         ext_rays++;
         Hit h2 = trace_closest<STATS>(sc, r2, p.seed, tc);
+        if (STATS && h2.gid != 0xffffffffu) tc.hits++;
         if (h2.gid == 0xffffffffu) miss<true>(cp, p);
         else closest_hit<STATS, true>(c, p, r2, h2, tc);
         acc = acc + p.color * thr;

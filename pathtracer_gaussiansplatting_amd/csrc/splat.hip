@@ -48,6 +48,8 @@ struct SplatWorkspace {
   DevBuf means2d, depths, conic, rgb, radii, touched, offsets, keys_in, vals_in, keys_out, vals_out, ranges, temp,
       point_keys, total;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
+  hipEvent_t ev[7] = {};
+  bool timed = false;
 };
 
 SplatWorkspace* splat_workspace_create() { return new SplatWorkspace(); }
@@ -58,6 +60,8 @@ void splat_workspace_destroy(SplatWorkspace* w) {
                    &w->vals_in, &w->keys_out, &w->vals_out, &w->ranges, &w->temp, &w->point_keys, &w->total};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
+  for (hipEvent_t& e : w->ev)
+    if (e) (void)hipEventDestroy(e);
   delete w;
 }
 
@@ -275,8 +279,14 @@ static uint32_t bits_for(uint32_t v) {
 
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
                            float p11, uint32_t W, uint32_t H, const float bg[3], uint32_t tile_row_begin,
-                           uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, hipStream_t s) {
+                           uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, bool time_stages,
+                           hipStream_t s) {
   hipError_t e;
+  if (time_stages && !w->ev[0])
+    for (hipEvent_t& ev : w->ev)
+      if ((e = hipEventCreate(&ev))) return e;
+  w->timed = time_stages;
+  auto mark = [&](int k) -> hipError_t { return time_stages ? hipEventRecord(w->ev[k], s) : hipSuccess; };
   const uint32_t n = g->count;
   SplatCam cam;
   std::memcpy(cam.view, view, sizeof(cam.view));
@@ -303,12 +313,14 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = ensure(w->ranges, (size_t)tiles * 8))) return e;
   if ((e = ensure(w->total, 16))) return e;
 
+  if ((e = mark(0))) return e;
   if (n) {
     hipLaunchKernelGGL(gs_preprocess_kernel, dim3((n + 255) / 256), dim3(256), 0, s, cam, g->means, g->scales,
                        g->rotations, g->opacities, g->colors, n, (float2*)w->means2d.p, (float*)w->depths.p,
                        (float4*)w->conic.p, (float4*)w->rgb.p, (int*)w->radii.p, (uint32_t*)w->touched.p);
     if ((e = hipGetLastError())) return e;
   }
+  if ((e = mark(1))) return e;
   // exclusive scan over n+1 entries (the last one = K)
   if ((e = hipMemsetAsync((uint32_t*)w->touched.p + n, 0, 4, s))) return e;
   size_t temp_bytes = 0;
@@ -319,6 +331,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = hipcub::DeviceScan::ExclusiveSum(w->temp.p, temp_bytes, (uint32_t*)w->touched.p, (uint32_t*)w->offsets.p,
                                             n + 1, s)))
     return e;
+  if ((e = mark(2))) return e;
   uint32_t K = 0;
   if ((e = hipMemcpyAsync(&K, (uint32_t*)w->offsets.p + n, 4, hipMemcpyDeviceToHost, s))) return e;
   if ((e = hipStreamSynchronize(s))) return e;
@@ -333,6 +346,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                        (const float2*)w->means2d.p, (const float*)w->depths.p, (const int*)w->radii.p,
                        (const uint32_t*)w->offsets.p, (unsigned long long*)w->keys_in.p, (uint32_t*)w->vals_in.p);
     if ((e = hipGetLastError())) return e;
+    if ((e = mark(3))) return e;
     int end_bit = 32 + (int)bits_for(tiles);
     size_t sort_bytes = 0;
     if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (unsigned long long*)w->keys_in.p,
@@ -344,10 +358,15 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                                                 (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_in.p,
                                                 (uint32_t*)w->vals_out.p, (int)K, 0, end_bit, s)))
       return e;
+    if ((e = mark(4))) return e;
     hipLaunchKernelGGL(gs_ranges_kernel, dim3((K + 255) / 256), dim3(256), 0, s, (const unsigned long long*)w->keys_out.p,
                        K, (uint2*)w->ranges.p);
     if ((e = hipGetLastError())) return e;
+  } else {
+    if ((e = mark(3))) return e;
+    if ((e = mark(4))) return e;
   }
+  if ((e = mark(5))) return e;
   uint32_t rows = cam.row_end - cam.row_begin;
   if (rows > 0) {
     hipLaunchKernelGGL(gs_blend_kernel, dim3(cam.grid_x, rows), dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p,
@@ -355,6 +374,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                        (const float4*)w->rgb.p, bg[0], bg[1], bg[2], (float4*)out);
     if ((e = hipGetLastError())) return e;
   }
+  if ((e = mark(6))) return e;
   w->last_n = n;
   w->last_k = K;
   w->last_tiles = tiles;
@@ -364,6 +384,16 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     stats->tiles_y = cam.grid_y;
     stats->num_visible = 0;
   }
+  return hipSuccess;
+}
+
+hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms) {
+  for (int k = 0; k < 6; ++k) out_ms[k] = 0.0f;
+  if (!w->timed || !w->ev[0]) return hipSuccess;
+  hipError_t e = hipEventSynchronize(w->ev[6]);
+  if (e) return e;
+  for (int k = 0; k < 6; ++k)
+    if ((e = hipEventElapsedTime(&out_ms[k], w->ev[k], w->ev[k + 1]))) return e;
   return hipSuccess;
 }
 

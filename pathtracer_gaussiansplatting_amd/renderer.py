@@ -137,6 +137,12 @@ class Renderer:
         self._chk(self.lib.ptgs_splat_get_buffers(self._h, C.byref(b)), "ptgs_splat_get_buffers")
         return b
 
+    def splat_stage_ms(self) -> np.ndarray:
+        """[preprocess, scan, duplicate, sort, ranges, blend] ms of the last splat (FLAG_TIME_STAGES)."""
+        out = np.zeros(6, np.float32)
+        self._chk(self.lib.ptgs_splat_stage_ms(self._h, _abi.fptr(out)), "ptgs_splat_stage_ms")
+        return out
+
     def encode_srgb8(self, rgba32f, width: int, height: int, rgba8, stream=None):
         rc = self.lib.ptgs_encode_srgb8(self._h, _ptr(rgba32f), width, height, _ptr(rgba8), _stream(stream))
         self._chk(rc, "ptgs_encode_srgb8")

@@ -1,0 +1,87 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol include/ptgs/*.h declares,
+struct layouts match the reference's (GeneralHeaders.h), and compute entry
+points fail loudly (no CPU fallback) when there is no device."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADERS = [os.path.join(ROOT, "include", "ptgs", f) for f in ("ptgs.h", "ptgs_host.h")]
+
+
+def _declared_functions():
+    names = set()
+    for h in HEADERS:
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"\b(ptgs_[a-z0-9_]+)\s*\(", text):
+            names.add(m.group(1))
+    return names
+
+
+def test_every_declared_symbol_is_exported(native_lib):
+    from pathtracer_gaussiansplatting_amd import _abi
+    declared = _declared_functions()
+    assert len(declared) >= 30
+    for name in sorted(declared):
+        assert hasattr(native_lib, name), f"{name} declared in include/ptgs but not exported"
+    # the Python mirror binds every declared symbol with a signature
+    assert declared == set(_abi.SYMBOLS), declared ^ set(_abi.SYMBOLS)
+
+
+def test_abi_version_and_arch(native_lib):
+    assert native_lib.ptgs_abi_version() == 1
+    assert native_lib.ptgs_device_arch() == b"gfx950"
+
+
+def test_struct_layouts():
+    from pathtracer_gaussiansplatting_amd import _abi
+    # Appendix B sizes / offsets
+    assert _abi.VERTEX_DTYPE.itemsize == 80
+    assert _abi.VERTEX_DTYPE.fields["normal"][1] == 16 and _abi.VERTEX_DTYPE.fields["tex_coord"][1] == 64
+    m = _abi.MATERIAL_DTYPE
+    assert m.itemsize == 308
+    assert m.fields["emissive_factor_and_pad"][1] == 208 and m.fields["metallic_factor"][1] == 224
+    assert m.fields["transmission_factor"][1] == 256 and m.fields["pad"][1] == 268
+    assert m.fields["albedo_texture_index"][1] == 272 and m.fields["sg_id"][1] == 300
+    assert m.fields["use_specular_glossiness_workflow"][1] == 304
+    assert C.sizeof(_abi.Ubo) == 192 and _abi.Ubo.frame_count.offset == 140 and _abi.Ubo.ambient_light.offset == 144
+    assert _abi.Ubo.emissive_flux.offset == 160 and _abi.Ubo.fov.offset == 176
+    assert _abi.PUNCTUAL_LIGHT_DTYPE.itemsize == 64 and _abi.PUNCTUAL_LIGHT_DTYPE.fields["type"][1] == 52
+    for dt in (_abi.MESH_INFO_DTYPE, _abi.LIGHT_TRIANGLE_DTYPE, _abi.LIGHT_CDF_DTYPE, _abi.PUNCTUAL_CDF_DTYPE):
+        assert dt.itemsize == 16
+    assert _abi.HITDATA_DTYPE.itemsize == 48 and _abi.HITDATA_DTYPE.fields["flag"][1] == 12
+    assert _abi.HITDATA_DTYPE.fields["normal"][1] == 32
+    assert C.sizeof(_abi.RayPush) == 80 and _abi.RayPush.mode.offset == 64 and _abi.RayPush.height.offset == 76
+
+
+def test_compute_path_fails_loudly_without_gpu(native_lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = C.c_void_p()
+    rc = native_lib.ptgs_create(0, C.byref(h))
+    assert rc == -2 and not h.value  # PTGS_EHIP: no device, no silent CPU path
+    from pathtracer_gaussiansplatting_amd import PtgsError, Renderer
+    with pytest.raises(PtgsError):
+        Renderer(0)
+
+
+def test_null_arguments_rejected(native_lib):
+    assert native_lib.ptgs_create(0, None) == -1
+    assert native_lib.ptgs_scene_upload(None, None) == -1
+    assert native_lib.ptgs_trace_camera(None, None, 1, 1, None, 1, 1, 0, None) == -1
+    assert native_lib.ptgs_mat4_inverse(None, None) == -1
+    z = np.zeros(16, np.float32)
+    out = np.zeros(16, np.float32)
+    from pathtracer_gaussiansplatting_amd._abi import fptr
+    assert native_lib.ptgs_mat4_inverse(fptr(z), fptr(out)) == -1  # singular
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from pathtracer_gaussiansplatting_amd import _abi
+    with pytest.raises(_abi.PtgsError):
+        _abi.load_library(str(tmp_path / "libptgs.so"))

@@ -1,0 +1,158 @@
+"""The CPU oracle on its own (no GPU): math primitives vs numpy, and size-independent properties of
+the restated algorithms (determinism, running-mean == per-frame RMW, SUM shards compose, row ranges
+partition a frame, 3DGS sort/range invariants and tile shards)."""
+import numpy as np
+import pytest
+
+import scenes_util as U
+from pathtracer_gaussiansplatting_amd import ACCUM_RUNNING_MEAN, ACCUM_SUM, Camera, make_ubo
+from pathtracer_gaussiansplatting_amd import synthetic as Y
+
+
+def test_sincos_accuracy(oracle_lib):
+    import ctypes as C
+    L = oracle_lib.lib()
+    xs = np.concatenate([np.linspace(0, 2 * np.pi, 4001), np.linspace(-20, 20, 2001)]).astype(np.float32)
+    s = C.c_float()
+    c = C.c_float()
+    err = 0.0
+    for x in xs:
+        L.oracle_sincos(float(x), C.byref(s), C.byref(c))
+        err = max(err, abs(s.value - np.sin(np.float64(x))), abs(c.value - np.cos(np.float64(x))))
+    assert err < 5e-7, err
+
+
+def test_exp2_log2_accuracy(oracle_lib):
+    L = oracle_lib.lib()
+    for x in np.linspace(-30, 30, 3001).astype(np.float32):
+        ref = 2.0 ** np.float64(x)
+        assert abs(L.oracle_exp2(float(x)) - ref) <= 4e-7 * ref
+    for x in np.geomspace(1e-6, 1e6, 3001).astype(np.float32):
+        assert abs(L.oracle_log2(float(x)) - np.log2(np.float64(x))) < 2e-6
+    assert L.oracle_exp2(-200.0) == 0.0
+
+
+def _render(oracle_lib, sc, ubo, W, H, spp, init=None, **kw):
+    acc = np.zeros((H, W, 4), np.float32) if init is None else init.copy()
+    st = oracle_lib.trace_camera(sc.desc(), ubo, W, H, acc, spp=spp, **kw)
+    return acc, st
+
+
+def test_running_mean_equals_per_frame(oracle_lib):
+    """spp=4 in one call == 4 calls of spp=1 with frame_count 0..3 (the reference's per-frame RMW)."""
+    sc = U.cornell()
+    pose = U.cornell_pose()
+    one, _ = _render(oracle_lib, sc, make_ubo(pose, sc, 0), 32, 32, 4)
+    acc = np.zeros((32, 32, 4), np.float32)
+    for f in range(4):
+        acc, _ = _render(oracle_lib, sc, make_ubo(pose, sc, f), 32, 32, 1, init=acc)
+    assert np.array_equal(one, acc)
+
+
+def test_sum_shards_compose(oracle_lib):
+    """§8e: G sample shards in SUM mode reduce to the same mean as one running-mean render (<1e-5)."""
+    sc = U.cornell()
+    pose = U.cornell_pose()
+    G, spp = 3, 2
+    total = np.zeros((24, 24, 4), np.float64)
+    for g in range(G):
+        part, _ = _render(oracle_lib, sc, make_ubo(pose, sc, g), 24, 24, spp, frame_stride=G, mode=ACCUM_SUM)
+        total += part
+    mean = total[..., :3] / total[..., 3:4]
+    ref, _ = _render(oracle_lib, sc, make_ubo(pose, sc, 0), 24, 24, G * spp)
+    assert np.all(total[..., 3] == G * spp)
+    assert U.rel_l2(mean, ref[..., :3]) < 1e-5
+
+
+def test_row_ranges_partition_frame(oracle_lib):
+    sc = U.cornell()
+    ubo = make_ubo(U.cornell_pose(), sc, 0)
+    full, sf = _render(oracle_lib, sc, ubo, 40, 30, 1)
+    a, sa = _render(oracle_lib, sc, ubo, 40, 30, 1, rows=(0, 13))
+    b, sb = _render(oracle_lib, sc, ubo, 40, 30, 1, rows=(13, 30))
+    assert np.array_equal(np.where(np.arange(30)[:, None, None] < 13, a, b), full)
+    assert sa.extension_rays + sb.extension_rays == sf.extension_rays
+    assert sa.shadow_rays + sb.shadow_rays == sf.shadow_rays
+
+
+def test_determinism_and_threads(oracle_lib):
+    sc = U.features()
+    ubo = make_ubo(U.cornell_pose(), sc, 5)
+    a, _ = _render(oracle_lib, sc, ubo, 48, 32, 2, threads=1)
+    b, _ = _render(oracle_lib, sc, ubo, 48, 32, 2, threads=4)
+    assert np.array_equal(a, b)
+
+
+def test_empty_scene_is_sky(oracle_lib, native_lib):
+    """no geometry: every primary ray misses -> colour = ambient * 2 (miss.rmiss:11-13)."""
+    from pathtracer_gaussiansplatting_amd import SceneBuilder
+    sc = SceneBuilder().finalize()
+    sc.blue_noise = U.blue_noise()
+    ubo = make_ubo(U.cornell_pose(), sc, 0, ambient=(0.1, 0.2, 0.3, 1.0))
+    acc, st = _render(oracle_lib, sc, ubo, 8, 8, 1)
+    assert np.allclose(acc[..., :3], [0.2, 0.4, 0.6])
+    assert st.extension_rays == 64 and st.shadow_rays == 0
+
+
+def _gs(oracle_lib, n, W, H, seed=3, **kw):
+    g = Y.gaussians_c2(n, seed=seed)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    return g, ubo, oracle_lib.splat_gaussians(g, ubo, W, H, **kw)
+
+
+def test_gs_sort_and_ranges_invariants(oracle_lib):
+    g, ubo, r = _gs(oracle_lib, 3000, 160, 90)
+    keys, vals, K = r["keys"], r["vals"], r["K"]
+    assert K == int(r["touched"].sum()) > 0
+    assert np.all(np.diff(keys.astype(np.uint64)) >= 0)  # sorted
+    tiles = (keys >> np.uint64(32)).astype(np.int64)
+    gx, gy = 10, 6
+    rng = r["ranges"].reshape(-1, 2)
+    for t in range(gx * gy):
+        s, e = rng[t]
+        assert np.all(tiles[s:e] == t)
+        assert e - s == np.count_nonzero(tiles == t)
+    # ties on (tile, depth) keep Gaussian order (stable)
+    same = np.flatnonzero(np.diff(keys.astype(np.uint64)) == 0)
+    assert np.all(vals[same] < vals[same + 1])
+    # depth bits in the key are the view depth of the Gaussian
+    d = (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32)
+    assert np.array_equal(d, r["depths"][vals])
+
+
+def test_gs_tile_shards_compose(oracle_lib):
+    _, _, full = _gs(oracle_lib, 2000, 120, 80, seed=4)
+    _, _, a = _gs(oracle_lib, 2000, 120, 80, seed=4, tile_rows=(0, 2))
+    _, _, b = _gs(oracle_lib, 2000, 120, 80, seed=4, tile_rows=(2, 5))
+    rows = np.arange(80)[:, None, None]
+    assert np.array_equal(np.where(rows < 32, a["image"], b["image"]), full["image"])
+    assert a["K"] + b["K"] == full["K"]
+
+
+def test_gs_against_python_loops(oracle_lib):
+    """Tiny case against an independent float64 pure-Python restatement of the blend (tolerance:
+    float32 vs float64 arithmetic)."""
+    g, ubo, r = _gs(oracle_lib, 40, 48, 32, seed=9)
+    img = np.zeros((32, 48, 3))
+    for py in range(32):
+        for px in range(48):
+            t = (py // 16) * 3 + (px // 16)
+            s, e = r["ranges"][2 * t], r["ranges"][2 * t + 1]
+            T, C = 1.0, np.zeros(3)
+            for j in range(s, e):
+                i = r["vals"][j]
+                dx = r["means2d"][2 * i] - px
+                dy = r["means2d"][2 * i + 1] - py
+                co = r["conic"][4 * i:4 * i + 4].astype(np.float64)
+                power = -0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy
+                if power > 0:
+                    continue
+                alpha = min(0.99, co[3] * np.exp(power))
+                if alpha < 1 / 255:
+                    continue
+                if T * (1 - alpha) < 1e-4:
+                    break
+                C += g["colors"][i] * alpha * T
+                T *= 1 - alpha
+            img[py, px] = C
+    assert np.max(np.abs(img - r["image"][..., :3])) < 1e-4
