@@ -185,7 +185,7 @@ def load_library(path: str | None = None) -> C.CDLL:
         import torch  # noqa: F401  (shares the HIP runtime)
     except Exception:
         pass
-    lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(p, mode=C.RTLD_GLOBAL if path is None else C.RTLD_LOCAL)
     for name, (res, args) in SYMBOLS.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -33,38 +33,42 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP toolchain is required to build libptgs.so")
 
 
-def _compile(src: str) -> str:
-    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+def _compile(src: str, defines: tuple = (), build_dir: str = BUILD) -> str:
+    obj = os.path.join(build_dir, os.path.basename(src) + ".o")
     path = os.path.join(CSRC, src)
     deps = [path] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     deps.append(os.path.join(INCLUDE, "ptgs", "ptgs.h"))
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj
-    cmd = [_hipcc()] + COMMON + [f"--offload-arch={ARCH}", "-c", path, "-o", obj]
+    dflags = [f"-D{d}" for d in defines]
+    cmd = [_hipcc()] + COMMON + dflags + [f"--offload-arch={ARCH}", "-c", path, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [_hipcc()] + COMMON + ["-x", "hip", f"--offload-arch={ARCH}", "-c", path, "-o", obj]
+        cmd = [_hipcc()] + COMMON + dflags + ["-x", "hip", f"--offload-arch={ARCH}", "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose: bool = False, defines: tuple = (), variant: str = "") -> str:
+    """Build libptgs.so (or, for A/B experiments, libptgs_<variant>.so with extra -D defines)."""
+    build_dir = BUILD if not variant else BUILD + "_" + variant
+    lib = LIB if not variant else os.path.join(HERE, f"libptgs_{variant}.so")
+    os.makedirs(build_dir, exist_ok=True)
     with ThreadPoolExecutor(max_workers=min(6, os.cpu_count() or 2)) as ex:
-        objs = list(ex.map(_compile, SOURCES))
-    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(o) for o in objs):
-        return LIB
-    tmp = LIB + ".tmp"
+        objs = list(ex.map(lambda s: _compile(s, tuple(defines), build_dir), SOURCES))
+    if os.path.exists(lib) and all(os.path.getmtime(lib) >= os.path.getmtime(o) for o in objs):
+        return lib
+    tmp = lib + ".tmp"
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
-        "-Wl,-rpath,/opt/rocm/lib", "-L/opt/rocm/lib", "-lamdhip64"]
+        "-Wl,-Bsymbolic", "-Wl,-rpath,/opt/rocm/lib", "-L/opt/rocm/lib", "-lamdhip64"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", lib)
+    return lib
 
 
 if __name__ == "__main__":

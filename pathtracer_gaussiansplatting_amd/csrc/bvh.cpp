@@ -81,8 +81,9 @@ struct Builder {
 
     uint32_t mid = begin + n / 2;
     bool split_found = false;
-    // past depth 32 only balanced splits: keeps the tree depth (= traversal stack bound) <= 32 + log2(n)
-    if (ext[axis] > 0.0f && d < 32) {
+    // past depth 20 only balanced splits: tree depth <= 20 + log2(n / 4) + 1 < 48 = the LDS traversal
+    // stack of the kernels (PTGS_STACK), for any n < 2^27
+    if (ext[axis] > 0.0f && d < 20) {
       const int NB = 32;
       float best_cost = std::numeric_limits<float>::infinity();
       int best_axis = -1, best_bin = -1;

@@ -64,7 +64,11 @@ struct TraversalCounters {
   uint32_t hits;   // closest hits (shaded surface points)
 };
 
-#define PTGS_STACK 64
+// Traversal stack: PTGS_STACK entries per work-item in LDS, interleaved across the 256 work-items
+// of a workgroup (entry k of lane t at [k * 256 + t]: conflict-free ds_read/ds_write_b32).
+// 48 x 256 x 4 B = 48 KiB per workgroup; the BVH builder bounds the tree depth below PTGS_STACK.
+#define PTGS_STACK 48
+#define PTGS_BLOCK 256
 
 PTGS_HD float i2f(int x) { union { int i; float f; } c; c.i = x; return c.f; }
 __device__ __forceinline__ int f2i(float x) { return __float_as_int(x); }
@@ -183,9 +187,9 @@ __device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, i
 }
 
 template <bool STATS>
-__device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, uint32_t seed, TraversalCounters& cnt) {
+__device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
+                                             TraversalCounters& cnt) {
   Hit h; h.t = r.tmax; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu; h.slot = 0;
-  int stack[PTGS_STACK];
   int sp = 0;
   int node = 0;
   while (true) {
@@ -199,7 +203,7 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
       if (h0 && h1) {
         int near = c0, far = c1;
         if (t1 < t0) { near = c1; far = c0; }
-        stack[sp++] = far;
+        stack[(sp++) * PTGS_BLOCK] = far;
         node = near;
       } else if (h0) {
         node = c0;
@@ -207,19 +211,19 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
         node = c1;
       } else {
         if (sp == 0) return h;
-        node = stack[--sp];
+        node = stack[(--sp) * PTGS_BLOCK];
       }
     }
     leaf_closest<STATS>(sc, r, node, h, seed, cnt);
     if (sp == 0) return h;
-    node = stack[--sp];
+    node = stack[(--sp) * PTGS_BLOCK];
   }
 }
 
 // any-hit: true if something blocks the segment [tmin, tmax]
 template <bool STATS>
-__device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint32_t seed, TraversalCounters& cnt) {
-  int stack[PTGS_STACK];
+__device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
+                                          TraversalCounters& cnt) {
   int sp = 0;
   int node = 0;
   while (true) {
@@ -233,7 +237,7 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
       if (h0 && h1) {
         int near = c0, far = c1;
         if (t1 < t0) { near = c1; far = c0; }
-        stack[sp++] = far;
+        stack[(sp++) * PTGS_BLOCK] = far;
         node = near;
       } else if (h0) {
         node = c0;
@@ -241,7 +245,7 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
         node = c1;
       } else {
         if (sp == 0) return false;
-        node = stack[--sp];
+        node = stack[(--sp) * PTGS_BLOCK];
       }
     }
     uint32_t L = (uint32_t)(~node);
@@ -260,7 +264,7 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
       return true;
     }
     if (sp == 0) return false;
-    node = stack[--sp];
+    node = stack[(--sp) * PTGS_BLOCK];
   }
 }
 
@@ -284,6 +288,7 @@ struct Payload {
 struct ShadeCtx {
   const DevScene* sc;
   const CamParams* cp;
+  int* stack;  // this work-item's LDS traversal stack (stride PTGS_BLOCK)
   uint32_t shadow_rays;
 };
 
@@ -375,7 +380,7 @@ template <bool STATS>
 __device__ __forceinline__ float trace_shadow_dist(ShadeCtx& c, v3 o, v3 d, float maxd, uint32_t seed, TraversalCounters& cnt) {
   c.shadow_rays++;
   Ray r = make_ray(o, d, 0.001f, maxd);
-  return trace_any<STATS>(*c.sc, r, seed, cnt) ? 0.0f : 1.0f;
+  return trace_any<STATS>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
 }
 
 // :119-126

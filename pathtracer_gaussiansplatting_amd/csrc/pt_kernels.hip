@@ -55,8 +55,12 @@ __device__ __forceinline__ float4 blue_noise_texel(const DevScene& sc, uint32_t 
   return sc.blue_noise[py * sc.bn_size + px];
 }
 
+#ifndef PTGS_PT_MIN_WAVES
+#define PTGS_PT_MIN_WAVES 1
+#endif
+
 template <bool STATS>
-__global__ __launch_bounds__(256) void pt_camera_kernel(DevScene sc, CamParams cp, float4* __restrict__ accum,
+__global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevScene sc, CamParams cp, float4* __restrict__ accum,
                                                         uint32_t W, uint32_t H, uint32_t row0, uint32_t row1,
                                                         uint32_t spp, uint32_t frame0, uint32_t stride,
                                                         uint32_t mode, unsigned long long* counters) {
@@ -66,7 +70,8 @@ __global__ __launch_bounds__(256) void pt_camera_kernel(DevScene sc, CamParams c
   const uint32_t y = row0 + blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
   const bool active = (x < W) && (y < row1);
 
-  ShadeCtx c; c.sc = &sc; c.cp = &cp; c.shadow_rays = 0;
+  __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
+  ShadeCtx c; c.sc = &sc; c.cp = &cp; c.stack = s_stack + threadIdx.x; c.shadow_rays = 0;
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
   uint32_t ext_rays = 0, samples = 0;
 
@@ -107,7 +112,7 @@ __global__ __launch_bounds__(256) void pt_camera_kernel(DevScene sc, CamParams c
         p.depth = depth;
         Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
         ext_rays++;
-        Hit h = trace_closest<STATS>(sc, ray, p.seed, tc);
+        Hit h = trace_closest<STATS>(sc, ray, p.seed, c.stack, tc);
         if (STATS && h.gid != 0xffffffffu) tc.hits++;
         if (h.gid == 0xffffffffu) miss<false>(cp, p);
         else closest_hit<STATS, false>(c, p, ray, h, tc);
@@ -150,7 +155,8 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
                                                        ptgs_hitdata* __restrict__ hits,
                                                        unsigned long long* counters) {
   const uint32_t index = blockIdx.x * blockDim.x + threadIdx.x;
-  ShadeCtx c; c.sc = &sc; c.cp = &cp; c.shadow_rays = 0;
+  __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
+  ShadeCtx c; c.sc = &sc; c.cp = &cp; c.stack = s_stack + threadIdx.x; c.shadow_rays = 0;
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
   uint32_t ext_rays = 0, nsamp = 0;
   if (index < n) {
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
 
     Ray ray = make_ray(so, rd, 0.0f, 10000.0f);
     ext_rays++;
-    Hit h = trace_closest<STATS>(sc, ray, p.seed, tc);
+    Hit h = trace_closest<STATS>(sc, ray, p.seed, c.stack, tc);
     if (STATS && h.gid != 0xffffffffu) tc.hits++;
     if (h.gid == 0xffffffffu) miss<true>(cp, p);
     else closest_hit<STATS, true>(c, p, ray, h, tc);
@@ -207,7 +213,7 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
         }
         Ray r2 = make_ray(p.next_o, p.next_d, 0.001f, 10000.0f);
         ext_rays++;
-        Hit h2 = trace_closest<STATS>(sc, r2, p.seed, tc);
+        Hit h2 = trace_closest<STATS>(sc, r2, p.seed, c.stack, tc);
         if (STATS && h2.gid != 0xffffffffu) tc.hits++;
         if (h2.gid == 0xffffffffu) miss<true>(cp, p);
         else closest_hit<STATS, true>(c, p, r2, h2, tc);

@@ -46,8 +46,8 @@ def _stream(stream) -> int:
 
 
 class Renderer:
-    def __init__(self, device: int = 0):
-        self.lib = _abi.load_library()
+    def __init__(self, device: int = 0, lib_path: str | None = None):
+        self.lib = _abi.load_library(lib_path)
         h = C.c_void_p()
         rc = self.lib.ptgs_create(int(device), C.byref(h))
         _abi.check(rc, f"ptgs_create(device={device})")

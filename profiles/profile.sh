@@ -1,0 +1,16 @@
+#!/bin/bash
+# Collect the rocprofv3 evidence for bench.py on a GPU box (run from the repo root via gpurun):
+#   pass 1: --kernel-trace --stats          (per-kernel durations; must agree with bench.py's HIP events)
+#   pass 2: --pmc FETCH_SIZE  (own pass)    (HBM read side; x2 on gfx950, MI355X_MICROARCH.md §HBM)
+#   pass 3: --pmc WRITE_SIZE  (own pass)    (HBM write side)
+# Outputs under gpurun_out/prof_<tag>/; summarise with profiles/parse_rocprof.py <tag>.
+set -euo pipefail
+TAG=${1:-r01}
+ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline"}
+OUT=gpurun_out/prof_${TAG}
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/kt" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_kt.log" 2>&1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/fetch" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_fetch.log" 2>&1
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/write" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_write.log" 2>&1
+echo "profiles collected in $OUT"
