@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/s (path trace) + Gsplats/s (3DGS) at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate
 
 
 def parse():
@@ -155,13 +156,18 @@ def main():
         rays_per_launch = rays_local / args.steps
         alg_bytes = bytes_per_ray * rays_per_launch
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        # HBM bytes per launch from the rocprof PMC passes of THIS library build (profiles/profile.sh +
+        # parse_rocprof.py record the sha256 of libptgs.so); null when the profile is stale or absent
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
         if os.path.exists(tpath):
             try:
+                import hashlib
                 tj = json.load(open(tpath))
                 e = tj.get("pt_camera_kernel", {})
-                if e.get("workload") == f"C3 {W}x{H} {SPP}spp {args.triangles}tri":
+                lib_sha = hashlib.sha256(open(os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", "libptgs.so"),
+                                              "rb").read()).hexdigest()
+                if e.get("workload") == f"C3 {W}x{H} {SPP}spp {args.triangles}tri" and tj.get("lib_sha256") == lib_sha:
                     traffic = e.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -180,7 +186,12 @@ def main():
                          "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
                          "bytes_per_ray": round(bytes_per_ray, 2),
                          "counts_per_ray": {"node_visits": cs.node_visits / max(rays_c, 1),
-                                            "tri_tests": cs.tri_tests / max(rays_c, 1)}},
+                                            "tri_tests": cs.tri_tests / max(rays_c, 1)},
+                         "note": "B_pt (SURVEY 8d) prices every BVH/triangle fetch at HBM; the C3 BVH is "
+                                 "L2/MALL-resident, so achieved can exceed the HBM peak; traffic = measured HBM "
+                                 "bytes per launch (rocprof, 2*FETCH_SIZE+WRITE_SIZE KiB)"},
+            "roofline_l2": {"bound": "l2", "achieved": round(achieved, 2), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(achieved / L2_PEAK_GBS, 5)},
         })
         del accum
 
@@ -233,7 +244,7 @@ def main():
         import oracle
         oracle.build()
         threads = min(16, os.cpu_count() or 1)
-        row_stride, spp_cpu = 2, 8  # ~10-30 s of CPU work on the box
+        row_stride, spp_cpu = 1, 16  # ~10-30 s of CPU work on the box
         acc = np.zeros((H, W, 4), np.float32)
         desc = scene.desc()
         cubo = make_ubo(pose, scene, 0, ambient=(0.3, 0.4, 0.5, 1.0), height=H)

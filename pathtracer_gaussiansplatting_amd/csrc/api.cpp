@@ -184,9 +184,9 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
 
   auto t0 = std::chrono::steady_clock::now();
   BvhOut bvh;
-  build_bvh(tris, 4, bvh);
+  build_bvh(tris, 4, PTGS_STACK - 1, bvh);
   auto t1 = std::chrono::steady_clock::now();
-  if (bvh.depth >= PTGS_STACK - 1) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
+  if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
 
   free_scene(c);
   c->info = ptgs_scene_info{};

@@ -39,6 +39,7 @@ struct Builder {
   std::vector<Ref> refs;
   std::vector<float>& nodes;
   int max_leaf;
+  uint32_t max_depth = 31;
   uint32_t depth = 0, max_leaf_seen = 0;
   float pad_abs;
 
@@ -81,9 +82,12 @@ struct Builder {
 
     uint32_t mid = begin + n / 2;
     bool split_found = false;
-    // past depth 20 only balanced splits: tree depth <= 20 + log2(n / 4) + 1 < 48 = the LDS traversal
-    // stack of the kernels (PTGS_STACK), for any n < 2^27
-    if (ext[axis] > 0.0f && d < 20) {
+    // Depth budget: SAH splits only while d + ceil(log2(n / leaf)) stays below max_depth; past that,
+    // balanced splits halve n per level, so the tree depth never exceeds max_depth (the kernels'
+    // LDS traversal stack, PTGS_STACK - 1).
+    uint32_t need = 0;
+    while (((uint64_t)max_leaf << need) < n) need++;
+    if (ext[axis] > 0.0f && d + need + 1 < max_depth) {
       const int NB = 32;
       float best_cost = std::numeric_limits<float>::infinity();
       int best_axis = -1, best_bin = -1;
@@ -162,12 +166,13 @@ struct Builder {
 
 }  // namespace
 
-void build_bvh(const std::vector<BuildTri>& tris, int max_leaf_size, BvhOut& out) {
+void build_bvh(const std::vector<BuildTri>& tris, int max_leaf_size, uint32_t max_depth, BvhOut& out) {
   out.nodes.clear();
   out.tris.clear();
   out.tri_flags.clear();
   max_leaf_size = std::max(1, std::min(16, max_leaf_size));
   Builder b(tris, out.nodes, max_leaf_size);
+  b.max_depth = max_depth;
   float maxabs = 0.0f;
   b.refs.resize(tris.size());
   for (size_t i = 0; i < tris.size(); ++i) {

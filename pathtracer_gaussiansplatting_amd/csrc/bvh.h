@@ -32,7 +32,7 @@ struct BvhOut {
   uint32_t max_leaf = 0;
 };
 
-// max_leaf_size <= 16
-void build_bvh(const std::vector<BuildTri>& tris, int max_leaf_size, BvhOut& out);
+// max_leaf_size <= 16; the tree depth is bounded by max_depth (>= log2(n / max_leaf_size) + 2)
+void build_bvh(const std::vector<BuildTri>& tris, int max_leaf_size, uint32_t max_depth, BvhOut& out);
 
 }  // namespace ptgs

@@ -66,8 +66,11 @@ struct TraversalCounters {
 
 // Traversal stack: PTGS_STACK entries per work-item in LDS, interleaved across the 256 work-items
 // of a workgroup (entry k of lane t at [k * 256 + t]: conflict-free ds_read/ds_write_b32).
-// 48 x 256 x 4 B = 48 KiB per workgroup; the BVH builder bounds the tree depth below PTGS_STACK.
-#define PTGS_STACK 48
+// 32 x 256 x 4 B = 32 KiB per workgroup (4 workgroups = 16 waves per CU fit the 160 KiB LDS); the
+// BVH builder bounds the tree depth below PTGS_STACK.
+#ifndef PTGS_STACK
+#define PTGS_STACK 32
+#endif
 #define PTGS_BLOCK 256
 
 PTGS_HD float i2f(int x) { union { int i; float f; } c; c.i = x; return c.f; }
@@ -97,6 +100,7 @@ __device__ __forceinline__ v3 ld3(const float* p) { return mk3(p[0], p[1], p[2])
 // ---------------------------------------------------------------------------------------------
 struct Ray {
   v3 o, d, inv;
+  v3 oinv;  // o * inv: slab distances as one FMA per plane (box tests need conservativeness only)
   float tmin, tmax;
 };
 
@@ -109,6 +113,7 @@ __device__ __forceinline__ float safe_inv(float d) {
 __device__ __forceinline__ Ray make_ray(v3 o, v3 d, float tmin, float tmax) {
   Ray r; r.o = o; r.d = d; r.tmin = tmin; r.tmax = tmax;
   r.inv = mk3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  r.oinv = mk3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
   return r;
 }
 
@@ -116,12 +121,23 @@ __device__ __forceinline__ Ray make_ray(v3 o, v3 d, float tmin, float tmax) {
 // test is conservative w.r.t. the triangle test's rounding.
 __device__ __forceinline__ void box2(const Ray& r, float4 n0, float4 n1, float4 n2, float tcap,
                                      bool& h0, bool& h1, float& t0, float& t1) {
+#ifdef PTGS_BOX_SUBMUL
   float ax0 = (n0.x - r.o.x) * r.inv.x, ax1 = (n0.y - r.o.x) * r.inv.x;
   float ay0 = (n0.z - r.o.y) * r.inv.y, ay1 = (n0.w - r.o.y) * r.inv.y;
   float az0 = (n2.x - r.o.z) * r.inv.z, az1 = (n2.y - r.o.z) * r.inv.z;
   float bx0 = (n1.x - r.o.x) * r.inv.x, bx1 = (n1.y - r.o.x) * r.inv.x;
   float by0 = (n1.z - r.o.y) * r.inv.y, by1 = (n1.w - r.o.y) * r.inv.y;
   float bz0 = (n2.z - r.o.z) * r.inv.z, bz1 = (n2.w - r.o.z) * r.inv.z;
+#else
+  // lo*inv - o*inv as one v_fma_f32 per plane; the host pads every box by >= 4e-7 x the scene's
+  // coordinate scale, which covers the extra rounding of o*inv (<= 6e-8 |o| in space).
+  float ax0 = __builtin_fmaf(n0.x, r.inv.x, -r.oinv.x), ax1 = __builtin_fmaf(n0.y, r.inv.x, -r.oinv.x);
+  float ay0 = __builtin_fmaf(n0.z, r.inv.y, -r.oinv.y), ay1 = __builtin_fmaf(n0.w, r.inv.y, -r.oinv.y);
+  float az0 = __builtin_fmaf(n2.x, r.inv.z, -r.oinv.z), az1 = __builtin_fmaf(n2.y, r.inv.z, -r.oinv.z);
+  float bx0 = __builtin_fmaf(n1.x, r.inv.x, -r.oinv.x), bx1 = __builtin_fmaf(n1.y, r.inv.x, -r.oinv.x);
+  float by0 = __builtin_fmaf(n1.z, r.inv.y, -r.oinv.y), by1 = __builtin_fmaf(n1.w, r.inv.y, -r.oinv.y);
+  float bz0 = __builtin_fmaf(n2.z, r.inv.z, -r.oinv.z), bz1 = __builtin_fmaf(n2.w, r.inv.z, -r.oinv.z);
+#endif
   float an = fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fmaxf(fminf(az0, az1), r.tmin));
   float af = fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fminf(fmaxf(az0, az1), tcap));
   float bn = fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fmaxf(fminf(bz0, bz1), r.tmin));

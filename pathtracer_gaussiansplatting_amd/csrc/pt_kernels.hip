@@ -55,8 +55,10 @@ __device__ __forceinline__ float4 blue_noise_texel(const DevScene& sc, uint32_t 
   return sc.blue_noise[py * sc.bn_size + px];
 }
 
+// 4 waves per SIMD (<= 128 VGPRs): measured +12% over the unconstrained 3-wave build (163 VGPRs)
+// despite ~150 B/lane of spills outside the traversal loop (tools/ab_pt.py, round 1).
 #ifndef PTGS_PT_MIN_WAVES
-#define PTGS_PT_MIN_WAVES 1
+#define PTGS_PT_MIN_WAVES 4
 #endif
 
 template <bool STATS>

@@ -75,14 +75,16 @@ def main(tag, workload):
         wa = sum(w) / len(w) if w else float("nan")
         hbm = (2 * fa + wa) * 1024
         lines.append(f"| {name[:90]} | {vg} | {fa:.1f} | {wa:.1f} | {hbm:.4g} |")
-        if "pt_camera_kernel" in name and (("<false>" in name) or ("<true>" not in name)):
+        if "pt_camera_kernel<false>" in name:
             traffic.setdefault("candidates", []).append({"name": name, "vgpr": vg, "hbm": hbm,
                                                          "fetch_kib": fa, "write_kib": wa})
-    # the timed (non-instrumented) pt kernel has the lower VGPR count
+    # the timed (non-instrumented) pt kernel is the <false> instantiation (profile.sh keeps full names)
     cands = traffic.get("candidates", [])
-    out = {"tag": tag}
+    import hashlib
+    lib = os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", "libptgs.so")
+    out = {"tag": tag, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest()}
     if cands:
-        c = min(cands, key=lambda c: int(c["vgpr"]) if str(c["vgpr"]).isdigit() else 1 << 30)
+        c = cands[0]
         out["pt_camera_kernel"] = {"workload": workload, "hbm_bytes_per_launch": c["hbm"], "vgpr": c["vgpr"],
                                    "fetch_kib": c["fetch_kib"], "write_kib": c["write_kib"],
                                    "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"}

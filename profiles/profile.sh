@@ -10,7 +10,7 @@ ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline"}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/kt" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_kt.log" 2>&1
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/fetch" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_fetch.log" 2>&1
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/write" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_write.log" 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_kt.log" 2>&1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_fetch.log" 2>&1
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_write.log" 2>&1
 echo "profiles collected in $OUT"
