@@ -47,7 +47,8 @@ struct DevBuf {
 struct SplatWorkspace {
   DevBuf means2d, depths, conic, rgb, radii, touched, pairs, keys_out, vals_out, ranges, tile_local, cursor,
       point_keys, total, rect, geo, hist, block_sum, block_off, ticket;
-  uint32_t* k_host = nullptr;  // pinned readback of K
+  uint32_t* k_host = nullptr;  // pinned, coherent: the scan kernel stores K here
+  uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
   hipEvent_t ev[7] = {};
@@ -236,7 +237,8 @@ __global__ __launch_bounds__(GS_SCAN_TILES) void gs_bin_scan_kernel(uint32_t* __
                                                                     uint32_t* __restrict__ block_sum,
                                                                     uint32_t* __restrict__ block_off,
                                                                     uint32_t* __restrict__ total,
-                                                                    uint32_t* __restrict__ ticket) {
+                                                                    uint32_t* __restrict__ ticket,
+                                                                    uint32_t* k_host) {
   __shared__ uint32_t s_v[GS_SCAN_TILES];
   __shared__ bool s_last;
   const uint32_t tid = threadIdx.x, t = blockIdx.x * GS_SCAN_TILES + tid;
@@ -289,6 +291,7 @@ __global__ __launch_bounds__(GS_SCAN_TILES) void gs_bin_scan_kernel(uint32_t* __
   }
   if (tid == 0) {
     *total = acc;
+    __atomic_store_n(k_host, acc, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
     *ticket = 0;  // ready for the next frame (stream order)
   }
 }
@@ -394,7 +397,7 @@ __device__ __forceinline__ void bitonic_flip_sort(uint32_t n, Swap swap_if) {
   }
 }
 
-#define GS_SORT_CAP 2048
+#define GS_SORT_CAP 1024
 
 // One 256-thread workgroup per 16x16 tile: sort the tile's pairs by (depth, gaussian) in LDS
 // (global memory for segments longer than GS_SORT_CAP), publish the sorted keys/values, then the
@@ -411,36 +414,71 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
                                                                  float4* __restrict__ out) {
   __shared__ unsigned long long s_key[GS_SORT_CAP];
   if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
-  __shared__ float4 s_ga[GS_BLOCK];  // (x, y, -a/2, -b)
-  __shared__ float4 s_gb[GS_BLOCK];  // (-c/2, log2 o, r, g)
-  __shared__ float s_gc[GS_BLOCK];   // b
-  __shared__ uint8_t s_list[4][GS_BLOCK];
+  // staged Gaussians of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads
+  // the per-quadrant lists to a multiple of 4
+  __shared__ float4 s_ga[GS_BLOCK + 1];  // (x, y, -a/2, -b)
+  __shared__ float4 s_gb[GS_BLOCK + 1];  // (-c/2, log2 o, r, g)
+  __shared__ float s_gc[GS_BLOCK + 1];   // b
+  __shared__ __attribute__((aligned(8))) uint16_t s_list[4][GS_BLOCK + 4];
   __shared__ uint32_t s_qcnt[4][4];  // [wave][quadrant]
   const uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
   const uint32_t tile = tile_y * cam.grid_x + tile_x;
   const uint32_t tid = threadIdx.x;
+  if (tid == 0) {
+    s_ga[GS_BLOCK] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    s_gb[GS_BLOCK] = make_float4(0.0f, -__builtin_huge_valf(), 0.0f, 0.0f);
+    s_gc[GS_BLOCK] = 0.0f;
+  }
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
+  const bool small = n <= GS_BLOCK;
   const bool in_lds = n <= GS_SORT_CAP;
   unsigned long long* seg = pairs + range.x;
-  if (in_lds) {
-    for (uint32_t k = tid; k < n; k += GS_BLOCK) s_key[k] = seg[k];
-    __syncthreads();
-    bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
-      unsigned long long x = s_key[a], y = s_key[b];
-      if (y < x) { s_key[a] = y; s_key[b] = x; }
-    });
-  } else {
-    bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
-      unsigned long long x = seg[a], y = seg[b];
-      if (y < x) { seg[a] = y; seg[b] = x; }
-    });
-  }
   const unsigned long long tbits = (unsigned long long)tile << 32;
-  for (uint32_t k = tid; k < n; k += GS_BLOCK) {
-    unsigned long long v = in_lds ? s_key[k] : seg[k];
-    keys_out[range.x + k] = tbits | (v >> 32);
-    vals_out[range.x + k] = (uint32_t)v;
+  unsigned long long my_key = ~0ull;  // small tiles: work-item tid holds sorted element tid
+  if (small) {
+    // one key per work-item: bitonic network in registers, lane exchanges by shuffle for strides
+    // < 64 and through LDS (two barriers) for the 64/128 strides only
+    if (tid < n) my_key = seg[tid];
+    uint32_t npad = 1;
+    while (npad < n) npad <<= 1;
+    for (uint32_t k = 2; k <= npad; k <<= 1)
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        unsigned long long other;
+        if (j >= 64) {
+          __syncthreads();
+          s_key[tid] = my_key;
+          __syncthreads();
+          other = s_key[tid ^ j];
+        } else {
+          other = __shfl_xor(my_key, (int)j);
+        }
+        const bool keep_min = ((tid & j) == 0) == ((tid & k) == 0);
+        my_key = keep_min ? (other < my_key ? other : my_key) : (other < my_key ? my_key : other);
+      }
+    if (tid < n) {
+      keys_out[range.x + tid] = tbits | (my_key >> 32);
+      vals_out[range.x + tid] = (uint32_t)my_key;
+    }
+  } else {
+    if (in_lds) {
+      for (uint32_t k = tid; k < n; k += GS_BLOCK) s_key[k] = seg[k];
+      __syncthreads();
+      bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
+        unsigned long long x = s_key[a], y = s_key[b];
+        if (y < x) { s_key[a] = y; s_key[b] = x; }
+      });
+    } else {
+      bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
+        unsigned long long x = seg[a], y = seg[b];
+        if (y < x) { seg[a] = y; seg[b] = x; }
+      });
+    }
+    for (uint32_t k = tid; k < n; k += GS_BLOCK) {
+      unsigned long long v = in_lds ? s_key[k] : seg[k];
+      keys_out[range.x + k] = tbits | (v >> 32);
+      vals_out[range.x + k] = (uint32_t)v;
+    }
   }
 
 #ifdef GS_PROBE_NO_BLEND
@@ -467,7 +505,7 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
     const uint32_t idx = base + tid;
     uint32_t m = 0;
     if (idx < n) {
-      const uint32_t g = (uint32_t)(in_lds ? s_key[idx] : seg[idx]);
+      const uint32_t g = small ? (uint32_t)my_key : (uint32_t)(in_lds ? s_key[idx] : seg[idx]);
       const float4 ge = geo[g], co = conic_o[g], c = rgb[g];
       s_ga[tid] = make_float4(ge.x, ge.y, -0.5f * co.x, -co.y);
       s_gb[tid] = make_float4(-0.5f * co.z, __log2f(co.w), c.x, c.y);
@@ -491,26 +529,43 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
       if ((m >> q) & 1u) {
         uint32_t off = rank[q];
         for (uint32_t w2 = 0; w2 < wave; ++w2) off += s_qcnt[w2][q];
-        s_list[q][off] = (uint8_t)tid;
+        s_list[q][off] = (uint16_t)tid;
       }
+#ifdef GS_PROBE_NO_EVAL
+    const uint32_t cnt = 0;
+#else
     const uint32_t cnt = s_qcnt[0][wave] + s_qcnt[1][wave] + s_qcnt[2][wave] + s_qcnt[3][wave];
+#endif
     __syncthreads();
-    for (uint32_t j = 0; !done && j < cnt; ++j) {
-      const uint32_t k = s_list[wave][j];
-      const float4 ga = s_ga[k];
-      const float dx = ga.x - pfx, dy = ga.y - pfy;
-      const float4 gb = s_gb[k];
-      const float power = __builtin_fmaf(__builtin_fmaf(ga.z, dx, ga.w * dy), dx, (gb.x * dy) * dy);
-      const float z = __builtin_fmaf(power, 1.4426950408889634f, gb.y);
-      if (power > 0.0f || z < -7.9943534f) continue;  // alpha < 1/255 (log2(1/255) = -7.99435)
-      const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(z));
-      const float test_T = T * (1.0f - alpha);
-      if (test_T < 0.0001f) { done = true; continue; }
-      const float wgt = alpha * T;
-      C0 = __builtin_fmaf(gb.z, wgt, C0);
-      C1 = __builtin_fmaf(gb.w, wgt, C1);
-      C2 = __builtin_fmaf(s_gc[k], wgt, C2);
-      T = test_T;
+    // wave-uniform trip count; the list is padded with the null Gaussian up to a multiple of 4
+    const uint32_t cntu = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
+    if (lane < 4) s_list[wave][cntu + lane] = (uint16_t)GS_BLOCK;
+    const uint16_t* list = s_list[wave];
+    for (uint32_t j = 0; j < cntu; j += 4) {
+      if (__ballot(!done) == 0) break;
+      const uint2 k4 = *reinterpret_cast<const uint2*>(list + j);  // 4 list entries
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = ((u < 2 ? k4.x : k4.y) >> (16 * (u & 1))) & 0xFFFFu;
+        const float4 ga = s_ga[k], gb = s_gb[k];
+        const float gcz = s_gc[k];
+        const float dx = ga.x - pfx, dy = ga.y - pfy;
+        const float power = __builtin_fmaf(__builtin_fmaf(ga.z, dx, ga.w * dy), dx, (gb.x * dy) * dy);
+        const float z = __builtin_fmaf(power, 1.4426950408889634f, gb.y);
+        // alpha >= 1/255 <=> z >= log2(1/255) = -7.99435; power > 0 is skipped as in the reference
+        const bool valid = !done && power <= 0.0f && z >= -7.9943534f;
+        float alpha = valid ? fminf(0.99f, __builtin_amdgcn_exp2f(z)) : 0.0f;
+        float test_T = T * (1.0f - alpha);
+        const bool term = valid && test_T < 0.0001f;  // saturated: stop before this Gaussian
+        done = done || term;
+        alpha = term ? 0.0f : alpha;
+        test_T = term ? T : test_T;
+        const float wgt = alpha * T;
+        C0 = __builtin_fmaf(gb.z, wgt, C0);
+        C1 = __builtin_fmaf(gb.w, wgt, C1);
+        C2 = __builtin_fmaf(gcz, wgt, C2);
+        T = test_T;
+      }
     }
   }
   if (inside) out[(size_t)py * cam.W + px] = make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T);
@@ -576,7 +631,10 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = ensure(w->hist, (size_t)nblk * tiles * 4))) return e;
   if (!lds_bins && (e = ensure(w->cursor, (size_t)tiles * 4))) return e;
   if ((e = ensure(w->total, 16))) return e;
-  if (!w->k_host && (e = hipHostMalloc((void**)&w->k_host, 16))) return e;
+  if (!w->k_host) {
+    if ((e = hipHostMalloc((void**)&w->k_host, 16, hipHostMallocCoherent | hipHostMallocMapped))) return e;
+    if ((e = hipHostGetDevicePointer((void**)&w->k_dev, w->k_host, 0))) return e;
+  }
   if (!w->k_event && (e = hipEventCreateWithFlags(&w->k_event, hipEventDisableTiming))) return e;
   // The pair buffer is sized from the previous frame's K (x1.25, at least 8 pairs per Gaussian) so
   // that scatter and blend are enqueued before K is known: the host then waits only for the small
@@ -617,9 +675,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   }
   hipLaunchKernelGGL(gs_bin_scan_kernel, dim3(scan_blocks), dim3(GS_SCAN_TILES), 0, s, (uint32_t*)w->hist.p, nblk,
                      tiles, (uint2*)w->tile_local.p, (uint32_t*)w->block_sum.p, (uint32_t*)w->block_off.p,
-                     (uint32_t*)w->total.p, (uint32_t*)w->ticket.p);
+                     (uint32_t*)w->total.p, (uint32_t*)w->ticket.p, w->k_dev);
   if ((e = hipGetLastError())) return e;
-  if ((e = hipMemcpyAsync(w->k_host, w->total.p, 4, hipMemcpyDeviceToHost, s))) return e;
   if ((e = hipEventRecord(w->k_event, s))) return e;
   if ((e = mark(2))) return e;
 

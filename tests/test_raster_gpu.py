@@ -36,7 +36,8 @@ def _gauss_ubo(W, H, g_scene=None):
 
 @pytest.mark.parametrize("n,W,H", [(2000, 160, 96), (20000, 320, 180), (0, 64, 64), (1, 33, 17),
                                    (3000, 3840, 2160),   # 32400 tiles: LDS histogram of 127 KiB
-                                   (500, 4104, 2160)])   # 34695 tiles: global-atomic binning fallback
+                                   (500, 4104, 2160),    # 34695 tiles: global-atomic binning fallback
+                                   (3000, 48, 40)])      # > GS_SORT_CAP pairs per tile: sort in global memory
 def test_gaussians_parity(renderer, oracle_lib, n, W, H):
     g = Y.gaussians_c2(n, seed=7)
     ubo = _gauss_ubo(W, H)

@@ -24,7 +24,8 @@ def main():
     for v in variants:
         path = os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", "libptgs.so" if v == "base" else f"libptgs_{v}.so")
         r = Renderer(0, lib_path=path)
-        r.set_flags(FLAG_TIME_STAGES)
+        if os.environ.get("GS_STAGES", "1") == "1":
+            r.set_flags(FLAG_TIME_STAGES)
         st = np.zeros(6)
         r.splat_gaussians(dg, ubo, W, H, img)
         torch.cuda.synchronize()
