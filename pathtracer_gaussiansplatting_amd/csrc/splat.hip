@@ -2,18 +2,21 @@
 //
 // The reference has no Gaussian rasterizer; this restates the published forward
 // pass (Kerbl et al., SIGGRAPH 2023) in the reference's camera conventions (glm::lookAt RH view,
-// Vulkan ZO projection with [1][1] negated, camera.cpp:186-187):
+// Vulkan ZO projection with [1][1] negated, camera.cpp:186-187). Four launches per frame:
 //   1. preprocess   one work-item per Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T,
-//                   EWA Sigma' = J W Sigma W^T J^T (+0.3 low-pass), conic, 3-sigma radius, tile rect
-//                   + per-tile pair counts (atomics)
-//   2. tile scan    one workgroup: per-tile [start, end) ranges, scatter cursors, K
-//   3. scatter      (depth bits << 32 | gaussian) into each touched tile's segment (atomic cursor)
-//   4. sort+blend   one 256-thread workgroup per 16x16 tile: bitonic sort of the tile's pairs by
-//                   (depth, gaussian) in LDS -> the same order as a stable global sort of
-//                   (tile << 32 | depth) keys; publish sorted keys/values; front-to-back alpha blend
-//                   with Gaussians staged through LDS in batches of 256, early exit at T < 1e-4
-// Integer outputs (radii, tiles, keys, ranges) are the bit-exact contract with
-// oracle/ptgs_oracle.c; the image is bit-identical as well (detmath exp, -ffp-contract=off).
+//                   EWA Sigma' = J W Sigma W^T J^T (+0.3 low-pass), conic, 3-sigma radius, tile rect,
+//                   a 48-B blend record
+//   2. count        (band of tile rows x chunk of Gaussians) workgroups: LDS tile histograms; the last
+//                   workgroup publishes the band offsets and K (to pinned host memory)
+//   3. scatter      same grid: band tile scan + chunk column offsets, then (depth << 32 | gaussian)
+//                   into each touched tile's segment through LDS cursors; tile ranges
+//   4. sort+blend   one workgroup per 16x16 tile: sort by (depth, gaussian) (= the order of a stable
+//                   global sort of (tile << 32 | depth) keys), publish keys/values, per-quadrant
+//                   culled front-to-back alpha blend
+// 3 and 4 are enqueued before K is read back (pair buffer sized from the previous frame, re-run on
+// growth), so the host never stalls the GPU. Integer outputs (radii, tiles, keys, values, ranges)
+// are the bit-exact contract with oracle/ptgs_oracle.c; the image is within 1e-4 relative L2
+// (hardware exp2 in the blend).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,8 +48,8 @@ struct DevBuf {
 };
 
 struct SplatWorkspace {
-  DevBuf means2d, depths, conic, rgb, radii, touched, pairs, keys_out, vals_out, ranges, tile_local, cursor,
-      point_keys, total, rect, geo, hist, block_sum, block_off, ticket;
+  DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, band_total,
+      band_off, point_keys, total, rect, ticket;
   uint32_t* k_host = nullptr;  // pinned, coherent: the scan kernel stores K here
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
@@ -59,9 +62,9 @@ SplatWorkspace* splat_workspace_create() { return new SplatWorkspace(); }
 
 void splat_workspace_destroy(SplatWorkspace* w) {
   if (!w) return;
-  DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rgb, &w->radii, &w->touched, &w->pairs, &w->keys_out,
-                   &w->vals_out, &w->ranges, &w->tile_local, &w->cursor, &w->point_keys, &w->total, &w->rect,
-                   &w->geo, &w->hist, &w->block_sum, &w->block_off, &w->ticket};
+  DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rec, &w->radii, &w->touched, &w->pairs, &w->keys_out,
+                   &w->vals_out, &w->ranges, &w->hist, &w->band_total, &w->band_off, &w->point_keys,
+                   &w->total, &w->rect, &w->ticket};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
@@ -90,19 +93,36 @@ __device__ __forceinline__ v4 mv4(const float* m, float x, float y, float z, flo
 
 __device__ __forceinline__ float ndc2pix(float v, int S) { return ((v + 1.0f) * (float)S - 1.0f) * 0.5f; }
 
-__global__ __launch_bounds__(256) void gs_preprocess_kernel(SplatCam cam, const float* __restrict__ means,
-                                                            const float* __restrict__ scales,
-                                                            const float* __restrict__ rots,
-                                                            const float* __restrict__ opac,
-                                                            const float* __restrict__ colors, uint32_t n,
-                                                            float2* __restrict__ means2d, float* __restrict__ depths,
-                                                            float4* __restrict__ conic_o, float4* __restrict__ rgb,
-                                                            int* __restrict__ radii, uint32_t* __restrict__ touched,
-                                                            ushort4* __restrict__ rects, float4* __restrict__ geo) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+struct PreArgs {
+  const float *means, *scales, *rots, *opac, *colors;
+  uint32_t n;
+  float2* means2d;
+  float* depths;
+  float4* conic_o;
+  int* radii;
+  uint32_t* touched;
+  ushort4* rects;
+  float4* rec;
+};
+
+// One Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T, EWA Sigma' = J W Sigma W^T J^T + 0.3,
+// conic, 3-sigma radius, tile rect, blend record.
+__device__ __forceinline__ void gs_preprocess_one(const SplatCam& cam, const PreArgs& A, uint32_t i) {
+  const float* __restrict__ means = A.means;
+  const float* __restrict__ scales = A.scales;
+  const float* __restrict__ rots = A.rots;
+  const float* __restrict__ opac = A.opac;
+  const float* __restrict__ colors = A.colors;
+  float2* __restrict__ means2d = A.means2d;
+  float* __restrict__ depths = A.depths;
+  float4* __restrict__ conic_o = A.conic_o;
+  int* __restrict__ radii = A.radii;
+  uint32_t* __restrict__ touched = A.touched;
+  ushort4* __restrict__ rects = A.rects;
+  float4* __restrict__ rec = A.rec;
   radii[i] = 0;
   touched[i] = 0;
+  rects[i] = make_ushort4(0, 0, 0, 0);  // empty rect: the scatter reads rects only
   float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   // frustum: view-space depth d = -z (RH, camera looks down -Z)
   v4 pv = mv4(cam.view, mx, my, mz, 1.0f);
@@ -173,20 +193,190 @@ __global__ __launch_bounds__(256) void gs_preprocess_kernel(SplatCam cam, const 
   radii[i] = r;
   means2d[i] = pimg;
   conic_o[i] = con;
-  // alpha = min(0.99, o * exp(power)) < 1/255  <=>  power < -ln(255 o). Pairs below that threshold
-  // minus a 1e-3 margin (>> the exp/log approximation error) are skipped without evaluating exp:
-  // the skipped set is a subset of the pairs the exact test rejects, so the image is unchanged.
-  float skip = -(log2x(255.0f * con.w) * 0.69314718055994531f) - 0.001f;
-  rgb[i] = make_float4(colors[3 * i], colors[3 * i + 1], colors[3 * i + 2], skip);
   touched[i] = (uint32_t)area;
   rects[i] = make_ushort4((unsigned short)rmin_x, (unsigned short)rmin_y, (unsigned short)rmax_x,
                           (unsigned short)rmax_y);
-  // half-extents of the ellipse power >= skip (q = d^T conic d <= -2 skip), +1% and +0.01 px margin;
-  // used only to skip whole 8x8 pixel blocks whose pairs the per-pixel skip test would reject anyway
-  float sq = -2.0f * skip;
-  float ex = sq > 0.0f ? sqrtx(sq * ca) * 1.01f + 0.01f : -1.0f;
-  float ey = sq > 0.0f ? sqrtx(sq * cc) * 1.01f + 0.01f : -1.0f;
-  geo[i] = make_float4(pimg.x, pimg.y, ex, ey);
+  // Blend record (3 x float4), the form the blend loop consumes:
+  //   (x, y, A, B), (C, log2 o, r, g), (b, ex, ey, 0)  with  A = -a/2 log2e, B = -b log2e, C = -c/2 log2e
+  // so that z = A dx^2 + B dx dy + C dy^2 + log2 o = power * log2e + log2 o and alpha = min(0.99, 2^z).
+  // (ex, ey): half-extents of the ellipse where alpha >= 1/255 can hold (power >= -ln(255 o), minus a
+  // 1e-3 margin, +1% and +0.01 px): the blend skips whole 8x8 pixel blocks outside that box.
+  const float L2E = 1.4426950408889634f;
+  const float skip = -(log2x(255.0f * con.w) * 0.69314718055994531f) - 0.001f;
+  const float sq = -2.0f * skip;
+  const float ex = sq > 0.0f ? sqrtx(sq * ca) * 1.01f + 0.01f : -1.0f;
+  const float ey = sq > 0.0f ? sqrtx(sq * cc) * 1.01f + 0.01f : -1.0f;
+  rec[3 * i] = make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E);
+  rec[3 * i + 1] = make_float4(-0.5f * con.z * L2E, __log2f(con.w), colors[3 * i], colors[3 * i + 1]);
+  rec[3 * i + 2] = make_float4(colors[3 * i + 2], ex, ey, 0.0f);
+}
+
+__global__ __launch_bounds__(256) void gs_preprocess_kernel(SplatCam cam, PreArgs A) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < A.n) gs_preprocess_one(cam, A, i);
+}
+
+// ---- binning --------------------------------------------------------------------------------------
+// No global atomics per pair (contended scattered atomics measured 100 us for C2's 617k pairs):
+// the grid is (bands, chunks): a band is a run of band_rows tile rows, a chunk a contiguous range
+// of Gaussians.
+//  count    block (band, c) counts the pairs of chunk c that fall in its band into an LDS histogram of
+//           the band's tiles (ds_add), writes it to hist[c][t] and adds its total to band_total[band];
+//           the last block to finish (ticket) turns the band totals into band offsets and K.
+//  scatter  block (band, c) recomputes its band's tile starts (band offset + scan of the band's tile
+//           totals) and its chunk's column offsets, then re-walks chunk c and places each pair at
+//           start[t] + sum_{c' < c} hist[c'][t] + (LDS cursor). Chunk-0 blocks publish the ranges.
+// Order inside a tile's segment depends on LDS atomic order and is fixed by the blend's per-tile sort.
+#define GS_BIN_THREADS 1024
+#define GS_BIN_CHUNKS 16
+#define GS_BIN_UNROLL 2
+#define GS_BAND_TILES 8192  // max tiles per band (LDS); W <= 131072 px
+
+struct BinGrid {
+  uint32_t band_rows, bands, chunks, chunk, grid_x, grid_y, tiles;
+};
+
+__device__ __forceinline__ void gs_band(const BinGrid& bg, uint32_t& ty0, uint32_t& ty1) {
+  ty0 = blockIdx.x * bg.band_rows;
+  ty1 = min(bg.grid_y, ty0 + bg.band_rows);
+}
+
+// walk chunk blockIdx.y's rects, GS_BIN_UNROLL loads in flight per work-item; f(i, rect, y0, y1) for
+// every Gaussian whose rect meets the band rows [ty0, ty1)
+template <typename F>
+__device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* __restrict__ rects, uint32_t n,
+                                              uint32_t ty0, uint32_t ty1, F f) {
+  const uint32_t b0 = blockIdx.y * bg.chunk, b1 = min(n, b0 + bg.chunk);
+  for (uint32_t base = b0 + threadIdx.x; base < b1; base += GS_BIN_THREADS * GS_BIN_UNROLL) {
+    ushort4 rc[GS_BIN_UNROLL];
+#pragma unroll
+    for (int u = 0; u < GS_BIN_UNROLL; ++u) {
+      const uint32_t i = base + u * GS_BIN_THREADS;
+      rc[u] = i < b1 ? rects[i] : make_ushort4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < GS_BIN_UNROLL; ++u) {
+      const uint32_t y0 = max((uint32_t)rc[u].y, ty0), y1 = min((uint32_t)rc[u].w, ty1);
+      if (y0 < y1 && rc[u].x < rc[u].z) f(base + u * GS_BIN_THREADS, rc[u], y0, y1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(BinGrid bg, const ushort4* __restrict__ rects,
+                                                                      uint32_t n, uint32_t* __restrict__ hist,
+                                                                      uint32_t* __restrict__ band_total,
+                                                                      uint32_t* __restrict__ band_off,
+                                                                      uint32_t* __restrict__ total,
+                                                                      uint32_t* __restrict__ ticket, uint32_t* k_host) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
+  __shared__ uint32_t s_sum[GS_BIN_THREADS / 64];
+  __shared__ bool s_last;
+  uint32_t ty0, ty1;
+  gs_band(bg, ty0, ty1);
+  const uint32_t nt = (ty1 - ty0) * bg.grid_x;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) s_hist[k] = 0;
+  __syncthreads();
+  gs_walk_chunk(bg, rects, n, ty0, ty1, [&](uint32_t, const ushort4& rc, uint32_t y0, uint32_t y1) {
+    for (uint32_t y = y0; y < y1; ++y)
+      for (uint32_t x = rc.x; x < rc.z; ++x) atomicAdd(s_hist + (y - ty0) * bg.grid_x + x, 1u);
+  });
+  __syncthreads();
+  uint32_t* row = hist + (size_t)blockIdx.y * bg.tiles + ty0 * bg.grid_x;
+  uint32_t part = 0;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) {
+    const uint32_t c = s_hist[k];
+    row[k] = c;
+    part += c;
+  }
+  for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+  if ((threadIdx.x & 63u) == 0) s_sum[threadIdx.x >> 6] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t blk = 0;
+    for (int w = 0; w < GS_BIN_THREADS / 64; ++w) blk += s_sum[w];
+    if (blk) atomicAdd(band_total + blockIdx.x, blk);
+    __builtin_amdgcn_s_waitcnt(0);  // the band-total add has been performed before the ticket
+    s_last = atomicAdd(ticket, 1u) == gridDim.x * gridDim.y - 1;
+  }
+  __syncthreads();
+  if (!s_last || threadIdx.x >= 64) return;
+  // last block, wave 0: band offsets (exclusive) and K; the band totals are read by exchange (where
+  // the adds were performed) and re-zeroed for the next frame; 64 bands per step, shuffle scan
+  const uint32_t lane = threadIdx.x;
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < bg.bands; b0 += 64) {
+    const uint32_t b = b0 + lane;
+    const uint32_t v = b < bg.bands ? atomicExch(band_total + b, 0u) : 0u;
+    uint32_t incl = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t u = __shfl_up(incl, off);
+      if ((int)lane >= off) incl += u;
+    }
+    if (b < bg.bands) band_off[b] = carry + incl - v;
+    carry += __shfl(incl, 63);
+  }
+  if (lane == 0) {
+    *total = carry;
+    __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
+    *ticket = 0;                                        // ready for the next frame (stream order)
+  }
+}
+
+// Pairs are written only when K fits the pair buffer (the host sizes it from the previous K and
+// re-runs scatter + blend after growing it when it did not: see splat_gaussians).
+__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
+    BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, uint32_t n,
+    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ band_off, const uint32_t* __restrict__ total,
+    uint32_t cap, uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];  // 2 * band_rows * grid_x
+  __shared__ uint32_t s_part[GS_BIN_THREADS];
+  if (*total > cap) return;
+  uint32_t ty0, ty1;
+  gs_band(bg, ty0, ty1);
+  const uint32_t nt = (ty1 - ty0) * bg.grid_x, t0 = ty0 * bg.grid_x;
+  uint32_t* s_tot = s_cur + nt;
+  const uint32_t c = blockIdx.y, tid = threadIdx.x;
+  // tile totals of the band and this chunk's column offsets
+  for (uint32_t k = tid; k < nt; k += GS_BIN_THREADS) {
+    uint32_t h[GS_BIN_CHUNKS];
+#pragma unroll
+    for (int r = 0; r < GS_BIN_CHUNKS; ++r) h[r] = r < (int)bg.chunks ? hist[(size_t)r * bg.tiles + t0 + k] : 0u;
+    uint32_t col = 0, tot = 0;
+#pragma unroll
+    for (int r = 0; r < GS_BIN_CHUNKS; ++r) {
+      col += r < (int)c ? h[r] : 0u;
+      tot += h[r];
+    }
+    s_cur[k] = col;
+    s_tot[k] = tot;
+  }
+  __syncthreads();
+  // exclusive scan of the band's tile totals: contiguous runs per work-item + Hillis-Steele
+  const uint32_t per = (nt + GS_BIN_THREADS - 1) / GS_BIN_THREADS;
+  const uint32_t kb = min(nt, tid * per), ke = min(nt, kb + per);
+  uint32_t local = 0;
+  for (uint32_t k = kb; k < ke; ++k) local += s_tot[k];
+  s_part[tid] = local;
+  __syncthreads();
+  for (uint32_t off = 1; off < GS_BIN_THREADS; off <<= 1) {
+    const uint32_t v = tid >= off ? s_part[tid - off] : 0u;
+    __syncthreads();
+    s_part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = band_off[blockIdx.x] + s_part[tid] - local;
+  for (uint32_t k = kb; k < ke; ++k) {
+    const uint32_t tot = s_tot[k];
+    if (c == 0) ranges[t0 + k] = tot ? make_uint2(run, run + tot) : make_uint2(0u, 0u);
+    s_cur[k] += run;
+    run += tot;
+  }
+  __syncthreads();
+  gs_walk_chunk(bg, rects, n, ty0, ty1, [&](uint32_t i, const ushort4& rc, uint32_t y0, uint32_t y1) {
+    const unsigned long long key = ((unsigned long long)__float_as_uint(depths[i]) << 32) | i;
+    for (uint32_t y = y0; y < y1; ++y)
+      for (uint32_t x = rc.x; x < rc.z; ++x) pairs[atomicAdd(s_cur + (y - ty0) * bg.grid_x + x, 1u)] = key;
+  });
 }
 
 // recompute the (clamped) rect of a visible Gaussian — same integer math as preprocess
@@ -198,178 +388,6 @@ __device__ __forceinline__ void gs_rect(const SplatCam& cam, float2 p, int r, in
   y0 = max(y0, (int)cam.row_begin);
   y1 = min(y1, (int)cam.row_end);
 }
-
-#define GS_BIN_THREADS 1024
-#define GS_SCAN_TILES 256
-
-// Binning without global atomics (scattered atomics run ~17x below the chip's atomic rate on
-// gfx950, MI355X_MICROARCH.md "Global float atomics"): block b of B owns a contiguous chunk of
-// Gaussians and counts its (gaussian, tile) pairs per tile in an LDS histogram (ds_add), written
-// block-major to hist[b][t]. gs_bin_scan_kernel turns the columns into per-block offsets and the
-// per-tile totals into tile starts; the scatter re-walks the same chunk and places each pair at
-// start[t] + hist[b][t] + (LDS cursor). The order inside a tile's segment depends on LDS atomic
-// order and is fixed by the blend kernel's per-tile sort.
-__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(const ushort4* __restrict__ rects,
-                                                                      const int* __restrict__ radii, uint32_t n,
-                                                                      uint32_t chunk, uint32_t tiles,
-                                                                      uint32_t grid_x, uint32_t* __restrict__ hist) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
-  for (uint32_t t = threadIdx.x; t < tiles; t += GS_BIN_THREADS) s_hist[t] = 0;
-  __syncthreads();
-  const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
-  for (uint32_t i = b0 + threadIdx.x; i < b1; i += GS_BIN_THREADS) {
-    if (radii[i] <= 0) continue;
-    ushort4 rc = rects[i];
-    for (uint32_t y = rc.y; y < rc.w; ++y)
-      for (uint32_t x = rc.x; x < rc.z; ++x) atomicAdd(s_hist + y * grid_x + x, 1u);
-  }
-  __syncthreads();
-  uint32_t* row = hist + (size_t)blockIdx.x * tiles;
-  for (uint32_t t = threadIdx.x; t < tiles; t += GS_BIN_THREADS) row[t] = s_hist[t];
-}
-
-// One work-item per tile: column scan of hist[.][t] (in place -> per-block offsets), the tile total
-// c, and a block-local exclusive scan of c over GS_SCAN_TILES tiles -> tile_local[t] = (prefix, c).
-// The last block to finish (ticket) scans the block sums -> block_off[] and K = total[0]; the tile
-// start is block_off[t / GS_SCAN_TILES] + tile_local[t].x (consumers add it themselves).
-__global__ __launch_bounds__(GS_SCAN_TILES) void gs_bin_scan_kernel(uint32_t* __restrict__ hist, uint32_t rows,
-                                                                    uint32_t tiles, uint2* __restrict__ tile_local,
-                                                                    uint32_t* __restrict__ block_sum,
-                                                                    uint32_t* __restrict__ block_off,
-                                                                    uint32_t* __restrict__ total,
-                                                                    uint32_t* __restrict__ ticket,
-                                                                    uint32_t* k_host) {
-  __shared__ uint32_t s_v[GS_SCAN_TILES];
-  __shared__ bool s_last;
-  const uint32_t tid = threadIdx.x, t = blockIdx.x * GS_SCAN_TILES + tid;
-  uint32_t run = 0;
-  if (t < tiles) {
-    for (uint32_t b0 = 0; b0 < rows; b0 += 16) {  // 16 independent loads in flight per lane
-      uint32_t c[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) c[k] = (b0 + k < rows) ? hist[(size_t)(b0 + k) * tiles + t] : 0u;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        if (b0 + k < rows) hist[(size_t)(b0 + k) * tiles + t] = run;
-        run += c[k];
-      }
-    }
-  }
-  s_v[tid] = run;
-  __syncthreads();
-  for (uint32_t off = 1; off < GS_SCAN_TILES; off <<= 1) {  // Hillis-Steele inclusive scan
-    uint32_t v = tid >= off ? s_v[tid - off] : 0u;
-    __syncthreads();
-    s_v[tid] += v;
-    __syncthreads();
-  }
-  if (t < tiles) tile_local[t] = make_uint2(s_v[tid] - run, run);
-  if (tid == GS_SCAN_TILES - 1) {
-    block_sum[blockIdx.x] = s_v[tid];
-    __threadfence();  // release the block sum before taking a ticket
-    s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();  // acquire the other blocks' sums
-  const uint32_t nb = gridDim.x;  // <= GS_LDS_TILES / GS_SCAN_TILES = 128 for the LDS path
-  uint32_t acc = 0;
-  for (uint32_t c0 = 0; c0 < nb; c0 += GS_SCAN_TILES) {
-    const uint32_t k = c0 + tid;
-    const uint32_t v0 = k < nb ? __atomic_load_n(block_sum + k, __ATOMIC_RELAXED) : 0u;
-    __syncthreads();
-    s_v[tid] = v0;
-    __syncthreads();
-    for (uint32_t off = 1; off < GS_SCAN_TILES; off <<= 1) {
-      uint32_t v = tid >= off ? s_v[tid - off] : 0u;
-      __syncthreads();
-      s_v[tid] += v;
-      __syncthreads();
-    }
-    if (k < nb) block_off[k] = acc + s_v[tid] - v0;
-    acc += s_v[GS_SCAN_TILES - 1];
-  }
-  if (tid == 0) {
-    *total = acc;
-    __atomic_store_n(k_host, acc, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
-    *ticket = 0;  // ready for the next frame (stream order)
-  }
-}
-
-__device__ __forceinline__ uint32_t gs_tile_start(const uint2* tile_local, const uint32_t* block_off, uint32_t t) {
-  return block_off[t / GS_SCAN_TILES] + tile_local[t].x;
-}
-
-// Pairs are written only when K fits the pair buffer (the host sizes it from the previous K and
-// re-runs scatter + blend after growing it when it did not: see splat_gaussians).
-__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
-    const ushort4* __restrict__ rects, const int* __restrict__ radii, const float* __restrict__ depths, uint32_t n,
-    uint32_t chunk, uint32_t tiles, uint32_t grid_x, const uint32_t* __restrict__ hist,
-    const uint2* __restrict__ tile_local, const uint32_t* __restrict__ block_off, const uint32_t* __restrict__ total,
-    uint32_t cap, uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
-  if (*total > cap) return;
-  const uint32_t* row = hist + (size_t)blockIdx.x * tiles;
-  for (uint32_t t = threadIdx.x; t < tiles; t += GS_BIN_THREADS) {
-    const uint2 tl = tile_local[t];
-    const uint32_t st = block_off[t / GS_SCAN_TILES] + tl.x;
-    s_cur[t] = st + row[t];
-    if (blockIdx.x == 0) ranges[t] = tl.y ? make_uint2(st, st + tl.y) : make_uint2(0u, 0u);
-  }
-  __syncthreads();
-  const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
-  for (uint32_t i = b0 + threadIdx.x; i < b1; i += GS_BIN_THREADS) {
-    if (radii[i] <= 0) continue;
-    ushort4 rc = rects[i];
-    unsigned long long key = ((unsigned long long)__float_as_uint(depths[i]) << 32) | i;
-    for (uint32_t y = rc.y; y < rc.w; ++y)
-      for (uint32_t x = rc.x; x < rc.z; ++x) {
-        uint32_t pos = atomicAdd(s_cur + y * grid_x + x, 1u);
-        pairs[pos] = key;
-      }
-  }
-}
-
-// Fallback for tile counts whose histogram does not fit LDS (> GS_LDS_TILES): global atomics into a
-// single histogram row (hist, zeroed), the same scan kernel, then global cursors (zeroed).
-__global__ __launch_bounds__(256) void gs_count_global_kernel(const ushort4* __restrict__ rects,
-                                                              const int* __restrict__ radii, uint32_t n,
-                                                              uint32_t grid_x, uint32_t* __restrict__ tile_count) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || radii[i] <= 0) return;
-  ushort4 rc = rects[i];
-  for (uint32_t y = rc.y; y < rc.w; ++y)
-    for (uint32_t x = rc.x; x < rc.z; ++x) atomicAdd(tile_count + y * grid_x + x, 1u);
-}
-
-__global__ __launch_bounds__(256) void gs_ranges_kernel(const uint2* __restrict__ tile_local,
-                                                        const uint32_t* __restrict__ block_off, uint32_t tiles,
-                                                        const uint32_t* __restrict__ total, uint32_t cap,
-                                                        uint2* __restrict__ ranges) {
-  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= tiles || *total > cap) return;
-  const uint2 tl = tile_local[t];
-  const uint32_t st = block_off[t / GS_SCAN_TILES] + tl.x;
-  ranges[t] = tl.y ? make_uint2(st, st + tl.y) : make_uint2(0u, 0u);
-}
-
-__global__ __launch_bounds__(256) void gs_scatter_global_kernel(
-    const ushort4* __restrict__ rects, const int* __restrict__ radii, const float* __restrict__ depths, uint32_t n,
-    uint32_t grid_x, const uint2* __restrict__ tile_local, const uint32_t* __restrict__ block_off,
-    const uint32_t* __restrict__ total, uint32_t cap, uint32_t* __restrict__ cursor,
-    unsigned long long* __restrict__ pairs) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || radii[i] <= 0 || *total > cap) return;
-  ushort4 rc = rects[i];
-  unsigned long long key = ((unsigned long long)__float_as_uint(depths[i]) << 32) | i;
-  for (uint32_t y = rc.y; y < rc.w; ++y)
-    for (uint32_t x = rc.x; x < rc.z; ++x) {
-      const uint32_t t = y * grid_x + x;
-      pairs[gs_tile_start(tile_local, block_off, t) + atomicAdd(cursor + t, 1u)] = key;
-    }
-}
-
-#define GS_LDS_TILES 32768
 
 // ascending bitonic sort ("flip" network: every comparator puts the min at the lower index) over
 // n elements; indices >= n act as +inf and are never touched, so n need not be a power of two.
@@ -397,49 +415,78 @@ __device__ __forceinline__ void bitonic_flip_sort(uint32_t n, Swap swap_if) {
   }
 }
 
-#define GS_SORT_CAP 1024
+#define GS_SORT_CAP 512
 
-// One 256-thread workgroup per 16x16 tile: sort the tile's pairs by (depth, gaussian) in LDS
-// (global memory for segments longer than GS_SORT_CAP), publish the sorted keys/values, then the
-// front-to-back alpha blend with Gaussians staged through LDS in batches of 256.
+struct GStage {  // one staged blend record (see gs_preprocess_kernel)
+  float4 a, b, c;
+};
+
+// One 256-work-item workgroup per 16x16 tile (a persistent, software-pipelined variant that loads
+// the next tile's keys during the current one measured slower: static tile assignment loses to the
+// dispatcher's dynamic balancing, 103 vs 72 us at C2).
+//  sort     the tile's pairs by (depth, gaussian): tiles of <= 256 pairs in registers (one key per
+//           work-item; while the network runs, the blend records of the unsorted keys are already
+//           in flight, the key carries its staging slot in its low 8 bits); larger tiles in LDS
+//           (global memory above GS_SORT_CAP) with records staged in batches of 256.
+//  publish  the sorted keys (tile << 32 | depth) / values (gaussian).
+//  blend    wave w shades the 8x8 quadrant q = w of the tile (x half w & 1, y half w >> 1), one pixel
+//           per lane. Each staged Gaussian's alpha box is tested against the four quadrants; a ballot
+//           + LDS offsets compact that into four ordered per-quadrant lists, so a wave iterates only
+//           the Gaussians that can touch its 64 pixels. alpha = min(0.99, 2^z) with the hardware exp2
+//           (within 1e-4 relative L2 of the oracle's exp, test_raster_gpu.py); front to back, stop
+//           before the Gaussian that would take T below 1e-4 (the reference's rule).
 __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, const uint2* __restrict__ ranges,
                                                                  unsigned long long* __restrict__ pairs,
                                                                  unsigned long long* __restrict__ keys_out,
                                                                  uint32_t* __restrict__ vals_out,
-                                                                 const float4* __restrict__ geo,
-                                                                 const float4* __restrict__ conic_o,
-                                                                 const float4* __restrict__ rgb, float bg_r,
+                                                                 const float4* __restrict__ rec, float bg_r,
                                                                  float bg_g, float bg_b,
                                                                  const uint32_t* __restrict__ total, uint32_t cap,
-                                                                 float4* __restrict__ out) {
+                                                                 uint32_t slot_keys, float4* __restrict__ out) {
   __shared__ unsigned long long s_key[GS_SORT_CAP];
-  if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
-  // staged Gaussians of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads
-  // the per-quadrant lists to a multiple of 4
-  __shared__ float4 s_ga[GS_BLOCK + 1];  // (x, y, -a/2, -b)
-  __shared__ float4 s_gb[GS_BLOCK + 1];  // (-c/2, log2 o, r, g)
-  __shared__ float s_gc[GS_BLOCK + 1];   // b
-  __shared__ __attribute__((aligned(8))) uint16_t s_list[4][GS_BLOCK + 4];
+  // staged records of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads the
+  // per-quadrant lists to a multiple of 4
+  __shared__ GStage s_stage[GS_BLOCK + 1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_list[4][GS_BLOCK + 4];  // byte offsets into s_stage
+  __shared__ uint8_t s_mask[GS_BLOCK];
   __shared__ uint32_t s_qcnt[4][4];  // [wave][quadrant]
+  if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   const uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
   const uint32_t tile = tile_y * cam.grid_x + tile_x;
-  const uint32_t tid = threadIdx.x;
+  const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
   if (tid == 0) {
-    s_ga[GS_BLOCK] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    s_gb[GS_BLOCK] = make_float4(0.0f, -__builtin_huge_valf(), 0.0f, 0.0f);
-    s_gc[GS_BLOCK] = 0.0f;
+    s_stage[GS_BLOCK].a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    s_stage[GS_BLOCK].b = make_float4(0.0f, -__builtin_huge_valf(), 0.0f, 0.0f);
+    s_stage[GS_BLOCK].c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
+  // quadrant mask of a record's alpha box: bit q = (x half q & 1, y half q >> 1)
+  auto quad_mask = [&](const float4& a, const float4& c) -> uint32_t {
+    const float x0 = a.x - c.y, x1 = a.x + c.y, y0 = a.y - c.z, y1 = a.y + c.z;
+    const bool xl = x0 <= tx0 + 7.0f && x1 >= tx0, xr = x0 <= tx0 + 15.0f && x1 >= tx0 + 8.0f;
+    const bool yt = y0 <= ty0 + 7.0f && y1 >= ty0, yb = y0 <= ty0 + 15.0f && y1 >= ty0 + 8.0f;
+    return (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
+           ((uint32_t)(xr && yb) << 3);
+  };
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
-  const bool small = n <= GS_BLOCK;
+  const bool small = slot_keys && n <= GS_BLOCK;
   const bool in_lds = n <= GS_SORT_CAP;
   unsigned long long* seg = pairs + range.x;
   const unsigned long long tbits = (unsigned long long)tile << 32;
-  unsigned long long my_key = ~0ull;  // small tiles: work-item tid holds sorted element tid
+  uint32_t my_slot = 0;  // small tiles: staging slot of sorted element tid
+  float4 ra, rb, rc;
+  unsigned long long key = ~0ull;
+  if (small && tid < n) {  // records are in flight while the network runs
+    const unsigned long long k_cur = seg[tid];
+    const uint32_t g = (uint32_t)k_cur;
+    ra = rec[3 * g];
+    rb = rec[3 * g + 1];
+    rc = rec[3 * g + 2];
+    key = (k_cur & 0xFFFFFFFF00000000ull) | ((unsigned long long)g << 8) | tid;  // g < 2^24 (slot_keys)
+  }
   if (small) {
-    // one key per work-item: bitonic network in registers, lane exchanges by shuffle for strides
-    // < 64 and through LDS (two barriers) for the 64/128 strides only
-    if (tid < n) my_key = seg[tid];
+    // bitonic network, one key per work-item: shuffles for strides < 64, LDS for 64 / 128
     uint32_t npad = 1;
     while (npad < n) npad <<= 1;
     for (uint32_t k = 2; k <= npad; k <<= 1)
@@ -447,18 +494,23 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
         unsigned long long other;
         if (j >= 64) {
           __syncthreads();
-          s_key[tid] = my_key;
+          s_key[tid] = key;
           __syncthreads();
           other = s_key[tid ^ j];
         } else {
-          other = __shfl_xor(my_key, (int)j);
+          other = __shfl_xor(key, (int)j);
         }
         const bool keep_min = ((tid & j) == 0) == ((tid & k) == 0);
-        my_key = keep_min ? (other < my_key ? other : my_key) : (other < my_key ? my_key : other);
+        key = keep_min ? (other < key ? other : key) : (other < key ? key : other);
       }
     if (tid < n) {
-      keys_out[range.x + tid] = tbits | (my_key >> 32);
-      vals_out[range.x + tid] = (uint32_t)my_key;
+      s_stage[tid].a = ra;
+      s_stage[tid].b = rb;
+      s_stage[tid].c = rc;
+      s_mask[tid] = (uint8_t)quad_mask(ra, rc);
+      keys_out[range.x + tid] = tbits | (key >> 32);
+      vals_out[range.x + tid] = (uint32_t)(key >> 8) & 0xFFFFFFu;
+      my_slot = (uint32_t)key & 0xFFu;
     }
   } else {
     if (in_lds) {
@@ -481,40 +533,33 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
     }
   }
 
-#ifdef GS_PROBE_NO_BLEND
-  return;
-#endif
-  // Blend. Wave w shades the 8x8 quadrant q = w of the tile (x half w & 1, y half w >> 1), one
-  // pixel per lane. Per batch of 256 sorted Gaussians staged in LDS, each work-item tests its
-  // Gaussian's skip-threshold ellipse box against the four quadrants; a ballot + LDS offsets compact
-  // that into four ordered per-quadrant lists, so a wave iterates only the Gaussians that can touch
-  // its 64 pixels. Per pair: alpha = min(0.99, 2^(power*log2e + log2 o)) with the hardware exp2
-  // (within 1e-4 relative L2 of the oracle's exp, test_raster_gpu.py).
-  const uint32_t wave = tid >> 6, lane = tid & 63u;
+#ifndef GS_PROBE_NO_BLEND
   const uint32_t px = tile_x * GS_BLOCK_X + (wave & 1u) * 8u + (lane & 7u);
   const uint32_t py = tile_y * GS_BLOCK_Y + (wave >> 1) * 8u + (lane >> 3);
-  const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
   const bool inside = px < cam.W && py < cam.H;
   bool done = !inside;
   const float pfx = (float)px, pfy = (float)py;
   float T = 1.0f;
   float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+  const char* stage = reinterpret_cast<const char*>(s_stage);
   int todo = (int)n;
   for (uint32_t base = 0; todo > 0; base += GS_BLOCK, todo -= GS_BLOCK) {
+    // (small tiles: the barrier also publishes the records and masks staged after the sort)
     if (__syncthreads_count(done) == GS_BLOCK) break;
     const uint32_t idx = base + tid;
-    uint32_t m = 0;
-    if (idx < n) {
-      const uint32_t g = small ? (uint32_t)my_key : (uint32_t)(in_lds ? s_key[idx] : seg[idx]);
-      const float4 ge = geo[g], co = conic_o[g], c = rgb[g];
-      s_ga[tid] = make_float4(ge.x, ge.y, -0.5f * co.x, -co.y);
-      s_gb[tid] = make_float4(-0.5f * co.z, __log2f(co.w), c.x, c.y);
-      s_gc[tid] = c.z;
-      const float x0 = ge.x - ge.z, x1 = ge.x + ge.z, y0 = ge.y - ge.w, y1 = ge.y + ge.w;
-      const bool xl = x0 <= tx0 + 7.0f && x1 >= tx0, xr = x0 <= tx0 + 15.0f && x1 >= tx0 + 8.0f;
-      const bool yt = y0 <= ty0 + 7.0f && y1 >= ty0, yb = y0 <= ty0 + 15.0f && y1 >= ty0 + 8.0f;
-      m = (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
-          ((uint32_t)(xr && yb) << 3);
+    uint32_t m = 0, slot = tid;
+    if (small) {
+      if (idx < n) {
+        slot = my_slot;
+        m = s_mask[slot];
+      }
+    } else if (idx < n) {
+      const uint32_t g = (uint32_t)(in_lds ? s_key[idx] : seg[idx]);
+      const float4 ga = rec[3 * g], gb = rec[3 * g + 1], gc = rec[3 * g + 2];
+      s_stage[tid].a = ga;
+      s_stage[tid].b = gb;
+      s_stage[tid].c = gc;
+      m = quad_mask(ga, gc);
     }
     uint32_t rank[4];
 #pragma unroll
@@ -529,7 +574,7 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
       if ((m >> q) & 1u) {
         uint32_t off = rank[q];
         for (uint32_t w2 = 0; w2 < wave; ++w2) off += s_qcnt[w2][q];
-        s_list[q][off] = (uint16_t)tid;
+        s_list[q][off] = slot * (uint32_t)sizeof(GStage);
       }
 #ifdef GS_PROBE_NO_EVAL
     const uint32_t cnt = 0;
@@ -539,36 +584,40 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
     __syncthreads();
     // wave-uniform trip count; the list is padded with the null Gaussian up to a multiple of 4
     const uint32_t cntu = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
-    if (lane < 4) s_list[wave][cntu + lane] = (uint16_t)GS_BLOCK;
-    const uint16_t* list = s_list[wave];
+    if (lane < 4) s_list[wave][cntu + lane] = GS_BLOCK * (uint32_t)sizeof(GStage);
+    const uint32_t* list = s_list[wave];
     for (uint32_t j = 0; j < cntu; j += 4) {
       if (__ballot(!done) == 0) break;
-      const uint2 k4 = *reinterpret_cast<const uint2*>(list + j);  // 4 list entries
+      const uint4 o4 = *reinterpret_cast<const uint4*>(list + j);  // 4 list entries
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint32_t k = ((u < 2 ? k4.x : k4.y) >> (16 * (u & 1))) & 0xFFFFu;
-        const float4 ga = s_ga[k], gb = s_gb[k];
-        const float gcz = s_gc[k];
-        const float dx = ga.x - pfx, dy = ga.y - pfy;
-        const float power = __builtin_fmaf(__builtin_fmaf(ga.z, dx, ga.w * dy), dx, (gb.x * dy) * dy);
-        const float z = __builtin_fmaf(power, 1.4426950408889634f, gb.y);
-        // alpha >= 1/255 <=> z >= log2(1/255) = -7.99435; power > 0 is skipped as in the reference
-        const bool valid = !done && power <= 0.0f && z >= -7.9943534f;
-        float alpha = valid ? fminf(0.99f, __builtin_amdgcn_exp2f(z)) : 0.0f;
-        float test_T = T * (1.0f - alpha);
-        const bool term = valid && test_T < 0.0001f;  // saturated: stop before this Gaussian
-        done = done || term;
-        alpha = term ? 0.0f : alpha;
-        test_T = term ? T : test_T;
-        const float wgt = alpha * T;
-        C0 = __builtin_fmaf(gb.z, wgt, C0);
-        C1 = __builtin_fmaf(gb.w, wgt, C1);
-        C2 = __builtin_fmaf(gcz, wgt, C2);
+        const uint32_t o = u == 0 ? o4.x : u == 1 ? o4.y : u == 2 ? o4.z : o4.w;
+        const float4 a = *reinterpret_cast<const float4*>(stage + o);
+        const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
+        const float cb = *reinterpret_cast<const float*>(stage + o + 32);
+        const float dx = a.x - pfx, dy = a.y - pfy;
+        // z = A dx^2 + B dx dy + C dy^2 + log2 o; the reference skips power > 0 (quadratic part > 0)
+        const float q2 = __builtin_fmaf(b.x * dy, dy, b.y);
+        const float z = __builtin_fmaf(__builtin_fmaf(a.z, dx, a.w * dy), dx, q2);
+        const bool valid = !done && z >= -7.9943534f && z <= b.y;  // alpha >= 1/255: z >= log2(1/255)
+        const float alpha = valid ? fminf(0.99f, __builtin_amdgcn_exp2f(z)) : 0.0f;
+        float wgt = alpha * T;
+        float test_T = T - wgt;
+        const bool term = test_T < 0.0001f;  // only a valid pair can get there
+        if (__ballot(term)) {  // rare: this Gaussian would saturate the pixel -> stop before it
+          done = done || term;
+          wgt = term ? 0.0f : wgt;
+          test_T = term ? T : test_T;
+        }
+        C0 = __builtin_fmaf(b.z, wgt, C0);
+        C1 = __builtin_fmaf(b.w, wgt, C1);
+        C2 = __builtin_fmaf(cb, wgt, C2);
         T = test_T;
       }
     }
   }
   if (inside) out[(size_t)py * cam.W + px] = make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T);
+#endif
 }
 
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
@@ -600,36 +649,32 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = ensure(w->means2d, (size_t)n * 8))) return e;
   if ((e = ensure(w->depths, (size_t)n * 4))) return e;
   if ((e = ensure(w->conic, (size_t)n * 16))) return e;
-  if ((e = ensure(w->rgb, (size_t)n * 16))) return e;
+  if ((e = ensure(w->rec, (size_t)n * 48))) return e;
   if ((e = ensure(w->radii, (size_t)n * 4))) return e;
   if ((e = ensure(w->touched, (size_t)n * 4))) return e;
-  if ((e = ensure(w->ranges, (size_t)tiles * 8))) return e;
-  if ((e = ensure(w->tile_local, (size_t)tiles * 8))) return e;
   if ((e = ensure(w->rect, (size_t)n * 8))) return e;
-  if ((e = ensure(w->geo, (size_t)n * 16))) return e;
-  const uint32_t scan_blocks = (tiles + GS_SCAN_TILES - 1) / GS_SCAN_TILES;
-  if ((e = ensure(w->block_sum, (size_t)scan_blocks * 4))) return e;
-  if ((e = ensure(w->block_off, (size_t)scan_blocks * 4))) return e;
+  if ((e = ensure(w->ranges, (size_t)tiles * 8))) return e;
+  // ~16 bands of tile rows x up to GS_BIN_CHUNKS chunks of Gaussians (~224 workgroups at 1080p)
+  if (cam.grid_x > GS_BAND_TILES) return hipErrorInvalidValue;  // W > 131072 px
+  BinGrid bgrid;
+  bgrid.grid_x = cam.grid_x;
+  bgrid.grid_y = cam.grid_y;
+  bgrid.tiles = tiles;
+  bgrid.band_rows = std::max(1u, std::min((cam.grid_y + 15u) / 16u, GS_BAND_TILES / cam.grid_x));
+  bgrid.bands = std::max(1u, (cam.grid_y + bgrid.band_rows - 1) / bgrid.band_rows);
+  bgrid.chunks = std::max(1u, std::min((uint32_t)GS_BIN_CHUNKS, (n + 4095u) / 4096u));
+  bgrid.chunk = std::max(1u, (n + bgrid.chunks - 1) / bgrid.chunks);
+  const size_t band_lds = (size_t)bgrid.band_rows * cam.grid_x * 4;
+  if ((e = ensure(w->hist, (size_t)bgrid.chunks * tiles * 4))) return e;
+  if ((e = ensure(w->band_off, (size_t)bgrid.bands * 4))) return e;
+  if (w->band_total.bytes < (size_t)bgrid.bands * 4) {  // zero once; the count re-zeroes it every frame
+    if ((e = ensure(w->band_total, (size_t)bgrid.bands * 4))) return e;
+    if ((e = hipMemset(w->band_total.p, 0, w->band_total.bytes))) return e;
+  }
   if (!w->ticket.p) {
     if ((e = ensure(w->ticket, 16))) return e;
     if ((e = hipMemset(w->ticket.p, 0, 16))) return e;
   }
-  const bool lds_bins = tiles <= GS_LDS_TILES;
-  static bool lds_attr_set = false;
-  if (lds_bins && !lds_attr_set) {  // the tile histogram may exceed the default 64 KiB dynamic LDS
-    if ((e = hipFuncSetAttribute((const void*)gs_bin_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 GS_LDS_TILES * 4)))
-      return e;
-    if ((e = hipFuncSetAttribute((const void*)gs_bin_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 GS_LDS_TILES * 4)))
-      return e;
-    lds_attr_set = true;
-  }
-  // histogram rows: enough blocks to spread the LDS atomics, few enough to keep the column scan short
-  const uint32_t nblk = lds_bins ? std::max(1u, std::min(64u, (n + 2047u) / 2048u)) : 1u;
-  const uint32_t chunk = (n + nblk - 1) / nblk;
-  if ((e = ensure(w->hist, (size_t)nblk * tiles * 4))) return e;
-  if (!lds_bins && (e = ensure(w->cursor, (size_t)tiles * 4))) return e;
   if ((e = ensure(w->total, 16))) return e;
   if (!w->k_host) {
     if ((e = hipHostMalloc((void**)&w->k_host, 16, hipHostMallocCoherent | hipHostMallocMapped))) return e;
@@ -651,53 +696,39 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   };
 
   if ((e = mark(0))) return e;
+  PreArgs pa;
+  pa.means = g->means;
+  pa.scales = g->scales;
+  pa.rots = g->rotations;
+  pa.opac = g->opacities;
+  pa.colors = g->colors;
+  pa.n = n;
+  pa.means2d = (float2*)w->means2d.p;
+  pa.depths = (float*)w->depths.p;
+  pa.conic_o = (float4*)w->conic.p;
+  pa.radii = (int*)w->radii.p;
+  pa.touched = (uint32_t*)w->touched.p;
+  pa.rects = (ushort4*)w->rect.p;
+  pa.rec = (float4*)w->rec.p;
   if (n) {
-    hipLaunchKernelGGL(gs_preprocess_kernel, dim3((n + 255) / 256), dim3(256), 0, s, cam, g->means, g->scales,
-                       g->rotations, g->opacities, g->colors, n, (float2*)w->means2d.p, (float*)w->depths.p,
-                       (float4*)w->conic.p, (float4*)w->rgb.p, (int*)w->radii.p, (uint32_t*)w->touched.p,
-                       (ushort4*)w->rect.p, (float4*)w->geo.p);
+    hipLaunchKernelGGL(gs_preprocess_kernel, dim3((n + 255) / 256), dim3(256), 0, s, cam, pa);
     if ((e = hipGetLastError())) return e;
   }
   if ((e = mark(1))) return e;
-  if (!n || !lds_bins) {
-    if ((e = hipMemsetAsync(w->hist.p, 0, (size_t)nblk * tiles * 4, s))) return e;
-    if (!lds_bins && (e = hipMemsetAsync(w->cursor.p, 0, (size_t)tiles * 4, s))) return e;
-  }
-  if (n && lds_bins) {
-    hipLaunchKernelGGL(gs_bin_count_kernel, dim3(nblk), dim3(GS_BIN_THREADS), tiles * 4, s,
-                       (const ushort4*)w->rect.p, (const int*)w->radii.p, n, chunk, tiles, cam.grid_x,
-                       (uint32_t*)w->hist.p);
-    if ((e = hipGetLastError())) return e;
-  } else if (n) {
-    hipLaunchKernelGGL(gs_count_global_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const ushort4*)w->rect.p,
-                       (const int*)w->radii.p, n, cam.grid_x, (uint32_t*)w->hist.p);
-    if ((e = hipGetLastError())) return e;
-  }
-  hipLaunchKernelGGL(gs_bin_scan_kernel, dim3(scan_blocks), dim3(GS_SCAN_TILES), 0, s, (uint32_t*)w->hist.p, nblk,
-                     tiles, (uint2*)w->tile_local.p, (uint32_t*)w->block_sum.p, (uint32_t*)w->block_off.p,
-                     (uint32_t*)w->total.p, (uint32_t*)w->ticket.p, w->k_dev);
+  // (n == 0: one chunk of nothing; the count still zeroes the band histograms and publishes K = 0)
+  hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), band_lds, s, bgrid,
+                     (const ushort4*)w->rect.p, n, (uint32_t*)w->hist.p, (uint32_t*)w->band_total.p,
+                     (uint32_t*)w->band_off.p, (uint32_t*)w->total.p, (uint32_t*)w->ticket.p, w->k_dev);
   if ((e = hipGetLastError())) return e;
   if ((e = hipEventRecord(w->k_event, s))) return e;
   if ((e = mark(2))) return e;
 
   const uint32_t rows = cam.row_end - cam.row_begin;
   auto enqueue_tail = [&](uint32_t cap) -> hipError_t {
-    if (lds_bins) {
-      hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(nblk), dim3(GS_BIN_THREADS), tiles * 4, s,
-                         (const ushort4*)w->rect.p, (const int*)w->radii.p, (const float*)w->depths.p, n, chunk,
-                         tiles, cam.grid_x, (const uint32_t*)w->hist.p, (const uint2*)w->tile_local.p,
-                         (const uint32_t*)w->block_off.p, (const uint32_t*)w->total.p, cap, (uint2*)w->ranges.p,
-                         (unsigned long long*)w->pairs.p);
-    } else {
-      hipLaunchKernelGGL(gs_ranges_kernel, dim3((tiles + 255) / 256), dim3(256), 0, s,
-                         (const uint2*)w->tile_local.p, (const uint32_t*)w->block_off.p, tiles,
-                         (const uint32_t*)w->total.p, cap, (uint2*)w->ranges.p);
-      if (n)
-        hipLaunchKernelGGL(gs_scatter_global_kernel, dim3((n + 255) / 256), dim3(256), 0, s,
-                           (const ushort4*)w->rect.p, (const int*)w->radii.p, (const float*)w->depths.p, n,
-                           cam.grid_x, (const uint2*)w->tile_local.p, (const uint32_t*)w->block_off.p,
-                           (const uint32_t*)w->total.p, cap, (uint32_t*)w->cursor.p, (unsigned long long*)w->pairs.p);
-    }
+    hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), 2 * band_lds, s,
+                       bgrid, (const ushort4*)w->rect.p, (const float*)w->depths.p, n, (const uint32_t*)w->hist.p,
+                       (const uint32_t*)w->band_off.p, (const uint32_t*)w->total.p, cap, (uint2*)w->ranges.p,
+                       (unsigned long long*)w->pairs.p);
     hipError_t e2 = hipGetLastError();
     if (e2) return e2;
     if ((e2 = mark(3))) return e2;
@@ -706,9 +737,9 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if (rows > 0) {
       hipLaunchKernelGGL(gs_sort_blend_kernel, dim3(cam.grid_x, rows), dim3(GS_BLOCK), 0, s, cam,
                          (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
-                         (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p, (const float4*)w->geo.p,
-                         (const float4*)w->conic.p, (const float4*)w->rgb.p, bg[0], bg[1], bg[2],
-                         (const uint32_t*)w->total.p, cap, (float4*)out);
+                         (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p, (const float4*)w->rec.p,
+                         bg[0], bg[1], bg[2], (const uint32_t*)w->total.p, cap, n < (1u << 24) ? 1u : 0u,
+                         (float4*)out);
       if ((e2 = hipGetLastError())) return e2;
     }
     return mark(6);
@@ -720,7 +751,6 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = ensure(w->pairs, (size_t)K * 8))) return e;
     if ((e = ensure(w->keys_out, (size_t)K * 8))) return e;
     if ((e = ensure(w->vals_out, (size_t)K * 4))) return e;
-    if (!lds_bins && (e = hipMemsetAsync(w->cursor.p, 0, (size_t)tiles * 4, s))) return e;
     if ((e = mark(2))) return e;
     if ((e = enqueue_tail(cap_now()))) return e;
   }

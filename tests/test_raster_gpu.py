@@ -1,7 +1,8 @@
 """Rasterizer + torus-tracer parity through the C-ABI (GPU) against the CPU oracle.
 
 3DGS (a11-a14): integer intermediates (radii, tiles touched, sorted keys/values, tile ranges) must
-be bit-exact; the image within 1e-4 relative L2 (bit-identical in practice). The 3DGS oracle follows
+be bit-exact; the image within 1e-4 relative L2 (the blend uses the hardware exp2; measured
+~1e-7, 4e-6 at 4K). The 3DGS oracle follows
 the published forward pass (the reference has none: parity unpinned w.r.t. the reference).
 """
 import ctypes as C
@@ -35,8 +36,8 @@ def _gauss_ubo(W, H, g_scene=None):
 
 
 @pytest.mark.parametrize("n,W,H", [(2000, 160, 96), (20000, 320, 180), (0, 64, 64), (1, 33, 17),
-                                   (3000, 3840, 2160),   # 32400 tiles: LDS histogram of 127 KiB
-                                   (500, 4104, 2160),    # 34695 tiles: global-atomic binning fallback
+                                   (3000, 3840, 2160),   # 32400 tiles (4K)
+                                   (500, 4104, 2160),    # 34695 tiles, ragged last tile column
                                    (3000, 48, 40)])      # > GS_SORT_CAP pairs per tile: sort in global memory
 def test_gaussians_parity(renderer, oracle_lib, n, W, H):
     g = Y.gaussians_c2(n, seed=7)
