@@ -49,7 +49,7 @@ struct DevBuf {
 
 struct SplatWorkspace {
   DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, band_total,
-      band_off, point_keys, total, rect, ticket;
+      band_off, tile_slots, point_keys, total, rect, ticket;
   uint32_t* k_host = nullptr;  // pinned, coherent: the scan kernel stores K here
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
@@ -63,7 +63,7 @@ SplatWorkspace* splat_workspace_create() { return new SplatWorkspace(); }
 void splat_workspace_destroy(SplatWorkspace* w) {
   if (!w) return;
   DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rec, &w->radii, &w->touched, &w->pairs, &w->keys_out,
-                   &w->vals_out, &w->ranges, &w->hist, &w->band_total, &w->band_off, &w->point_keys,
+                   &w->vals_out, &w->ranges, &w->hist, &w->band_total, &w->band_off, &w->tile_slots, &w->point_keys,
                    &w->total, &w->rect, &w->ticket};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
@@ -231,6 +231,7 @@ __global__ __launch_bounds__(256) void gs_preprocess_kernel(SplatCam cam, PreArg
 #define GS_BIN_CHUNKS 16
 #define GS_BIN_UNROLL 2
 #define GS_BAND_TILES 8192  // max tiles per band (LDS); W <= 131072 px
+#define GS_TILE_SLOTS 256   // fixed key slots per tile (= the register-sort limit)
 
 struct BinGrid {
   uint32_t band_rows, bands, chunks, chunk, grid_x, grid_y, tiles;
@@ -276,10 +277,12 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(BinGrid bg
   const uint32_t nt = (ty1 - ty0) * bg.grid_x;
   for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) s_hist[k] = 0;
   __syncthreads();
+#ifndef GS_PROBE_NO_WALK
   gs_walk_chunk(bg, rects, n, ty0, ty1, [&](uint32_t, const ushort4& rc, uint32_t y0, uint32_t y1) {
     for (uint32_t y = y0; y < y1; ++y)
       for (uint32_t x = rc.x; x < rc.z; ++x) atomicAdd(s_hist + (y - ty0) * bg.grid_x + x, 1u);
   });
+#endif
   __syncthreads();
   uint32_t* row = hist + (size_t)blockIdx.y * bg.tiles + ty0 * bg.grid_x;
   uint32_t part = 0;
@@ -327,7 +330,8 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(BinGrid bg
 __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, uint32_t n,
     const uint32_t* __restrict__ hist, const uint32_t* __restrict__ band_off, const uint32_t* __restrict__ total,
-    uint32_t cap, uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs) {
+    uint32_t cap, uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs,
+    unsigned long long* __restrict__ tile_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];  // 2 * band_rows * grid_x
   __shared__ uint32_t s_part[GS_BIN_THREADS];
   if (*total > cap) return;
@@ -368,14 +372,27 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
   for (uint32_t k = kb; k < ke; ++k) {
     const uint32_t tot = s_tot[k];
     if (c == 0) ranges[t0 + k] = tot ? make_uint2(run, run + tot) : make_uint2(0u, 0u);
-    s_cur[k] += run;
+    // s_cur: this chunk's next slot inside the tile; s_tot -> where the tile's pairs go: its fixed
+    // GS_TILE_SLOTS-slot row when they fit (the blend then loads keys without waiting for the range),
+    // else its segment of the pair buffer (flag bit 31)
+    s_tot[k] = tot <= GS_TILE_SLOTS ? (t0 + k) * GS_TILE_SLOTS : (run | 0x80000000u);
     run += tot;
   }
   __syncthreads();
+#ifdef GS_PROBE_NO_WALK
+  return;
+#endif
   gs_walk_chunk(bg, rects, n, ty0, ty1, [&](uint32_t i, const ushort4& rc, uint32_t y0, uint32_t y1) {
     const unsigned long long key = ((unsigned long long)__float_as_uint(depths[i]) << 32) | i;
     for (uint32_t y = y0; y < y1; ++y)
-      for (uint32_t x = rc.x; x < rc.z; ++x) pairs[atomicAdd(s_cur + (y - ty0) * bg.grid_x + x, 1u)] = key;
+      for (uint32_t x = rc.x; x < rc.z; ++x) {
+        const uint32_t k = (y - ty0) * bg.grid_x + x;
+        const uint32_t rel = atomicAdd(s_cur + k, 1u), dst = s_tot[k];
+        if (dst & 0x80000000u)
+          pairs[(dst & 0x7FFFFFFFu) + rel] = key;
+        else
+          tile_slots[dst + rel] = key;
+      }
   });
 }
 
@@ -442,7 +459,9 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
                                                                  const float4* __restrict__ rec, float bg_r,
                                                                  float bg_g, float bg_b,
                                                                  const uint32_t* __restrict__ total, uint32_t cap,
-                                                                 uint32_t slot_keys, float4* __restrict__ out) {
+                                                                 uint32_t slot_keys,
+                                                                 const unsigned long long* __restrict__ tile_slots,
+                                                                 float4* __restrict__ out) {
   __shared__ unsigned long long s_key[GS_SORT_CAP];
   // staged records of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads the
   // per-quadrant lists to a multiple of 4
@@ -468,27 +487,42 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
     return (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
            ((uint32_t)(xr && yb) << 3);
   };
+  // the tile's slot row is loaded together with its range (no dependent round trip for small tiles)
+  const unsigned long long k_slot = tile_slots[(size_t)tile * GS_TILE_SLOTS + tid];
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
   const bool small = slot_keys && n <= GS_BLOCK;
   const bool in_lds = n <= GS_SORT_CAP;
-  unsigned long long* seg = pairs + range.x;
+  // where the scatter put this tile's keys: its slot row (<= GS_TILE_SLOTS) or its pair segment
+  unsigned long long* seg = n <= GS_TILE_SLOTS
+                                ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
+                                : pairs + range.x;
   const unsigned long long tbits = (unsigned long long)tile << 32;
   uint32_t my_slot = 0;  // small tiles: staging slot of sorted element tid
   float4 ra, rb, rc;
   unsigned long long key = ~0ull;
   if (small && tid < n) {  // records are in flight while the network runs
-    const unsigned long long k_cur = seg[tid];
+    const unsigned long long k_cur = k_slot;
     const uint32_t g = (uint32_t)k_cur;
+#ifdef GS_PROBE_NO_REC
+    ra = rb = rc = make_float4((float)g, 0.f, 0.f, 0.f);
+#else
     ra = rec[3 * g];
     rb = rec[3 * g + 1];
     rc = rec[3 * g + 2];
+#endif
     key = (k_cur & 0xFFFFFFFF00000000ull) | ((unsigned long long)g << 8) | tid;  // g < 2^24 (slot_keys)
   }
   if (small) {
     // bitonic network, one key per work-item: shuffles for strides < 64, LDS for 64 / 128
     uint32_t npad = 1;
     while (npad < n) npad <<= 1;
+#ifdef GS_PROBE_NO_SORT
+    npad = 1;
+#endif
+    // waves wholly above npad hold only padding and skip the exchanges (they still join the
+    // barriers of the 64 / 128 strides)
+    const bool active = wave * 64u < npad;
     for (uint32_t k = 2; k <= npad; k <<= 1)
       for (uint32_t j = k >> 1; j > 0; j >>= 1) {
         unsigned long long other;
@@ -498,10 +532,11 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
           __syncthreads();
           other = s_key[tid ^ j];
         } else {
+          if (!active) continue;
           other = __shfl_xor(key, (int)j);
         }
-        const bool keep_min = ((tid & j) == 0) == ((tid & k) == 0);
-        key = keep_min ? (other < key ? other : key) : (other < key ? key : other);
+        const bool swap = (other < key) == (((tid & j) == 0) == ((tid & k) == 0));
+        key = swap ? other : key;
       }
     if (tid < n) {
       s_stage[tid].a = ra;
@@ -596,10 +631,11 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
         const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
         const float cb = *reinterpret_cast<const float*>(stage + o + 32);
         const float dx = a.x - pfx, dy = a.y - pfy;
-        // z = A dx^2 + B dx dy + C dy^2 + log2 o; the reference skips power > 0 (quadratic part > 0)
+        // z = A dx^2 + B dx dy + C dy^2 + log2 o. (The reference's power > 0 skip is not tested: the
+        // conic is positive definite (+0.3 low-pass), so power <= 0 up to rounding at power ~ 0.)
         const float q2 = __builtin_fmaf(b.x * dy, dy, b.y);
         const float z = __builtin_fmaf(__builtin_fmaf(a.z, dx, a.w * dy), dx, q2);
-        const bool valid = !done && z >= -7.9943534f && z <= b.y;  // alpha >= 1/255: z >= log2(1/255)
+        const bool valid = !done && z >= -7.9943534f;  // alpha >= 1/255: z >= log2(1/255)
         const float alpha = valid ? fminf(0.99f, __builtin_amdgcn_exp2f(z)) : 0.0f;
         float wgt = alpha * T;
         float test_T = T - wgt;
@@ -666,6 +702,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   bgrid.chunk = std::max(1u, (n + bgrid.chunks - 1) / bgrid.chunks);
   const size_t band_lds = (size_t)bgrid.band_rows * cam.grid_x * 4;
   if ((e = ensure(w->hist, (size_t)bgrid.chunks * tiles * 4))) return e;
+  if ((e = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e;
   if ((e = ensure(w->band_off, (size_t)bgrid.bands * 4))) return e;
   if (w->band_total.bytes < (size_t)bgrid.bands * 4) {  // zero once; the count re-zeroes it every frame
     if ((e = ensure(w->band_total, (size_t)bgrid.bands * 4))) return e;
@@ -728,7 +765,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), 2 * band_lds, s,
                        bgrid, (const ushort4*)w->rect.p, (const float*)w->depths.p, n, (const uint32_t*)w->hist.p,
                        (const uint32_t*)w->band_off.p, (const uint32_t*)w->total.p, cap, (uint2*)w->ranges.p,
-                       (unsigned long long*)w->pairs.p);
+                       (unsigned long long*)w->pairs.p, (unsigned long long*)w->tile_slots.p);
     hipError_t e2 = hipGetLastError();
     if (e2) return e2;
     if ((e2 = mark(3))) return e2;
@@ -739,7 +776,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                          (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
                          (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p, (const float4*)w->rec.p,
                          bg[0], bg[1], bg[2], (const uint32_t*)w->total.p, cap, n < (1u << 24) ? 1u : 0u,
-                         (float4*)out);
+                         (const unsigned long long*)w->tile_slots.p, (float4*)out);
       if ((e2 = hipGetLastError())) return e2;
     }
     return mark(6);
