@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PTGS_ABI_VERSION 1
+#define PTGS_ABI_VERSION 2
 
 /* ---------------- error codes ---------------- */
 #define PTGS_OK 0
@@ -171,6 +171,21 @@ typedef struct ptgs_ray_push {
  * it in the BLAS geometry, so it travels beside MeshInfo here. Meshes with fewer than 3
  * indices are skipped exactly like buildBlas does.
  * The context copies everything; the caller keeps ownership. */
+/* One texture of global_textures[] (binding 14, raytracing.glsl:138): RGBA8 level 0. The library
+ * builds the mip chain as Image::generateMipmaps does (image.cpp:203-290: linear blits, each level
+ * max(1, w/2) x max(1, h/2), floor(log2(max(w, h))) + 1 levels, image.cpp:35) and samples it as the
+ * reference's sampler does (image.cpp:124-138: linear min/mag/mip filtering, repeat addressing,
+ * LOD clamped to the chain). Formats follow Gameobject::scanTextureFormats (gameobject.cpp:284-345):
+ * base colour, emissive, spec-gloss and diffuse are sRGB; normal, metal-rough, occlusion, clearcoat
+ * and transmission UNORM. Material texture indices index this array (0 = the default white). */
+typedef struct ptgs_texture {
+    const uint8_t* rgba8; /* width * height * 4 bytes, row-major; row 0 holds v in [0, 1/height) */
+    uint32_t width;
+    uint32_t height;
+    uint32_t srgb;        /* 1 = VK_FORMAT_R8G8B8A8_SRGB, 0 = VK_FORMAT_R8G8B8A8_UNORM */
+    uint32_t reserved;
+} ptgs_texture;
+
 typedef struct ptgs_scene_desc {
     const ptgs_vertex* vertices;
     uint32_t num_vertices;
@@ -193,6 +208,9 @@ typedef struct ptgs_scene_desc {
      * values already decoded with the stbi_loadf convention (RGB^2.2, A linear). */
     const float* blue_noise_rgba32f;
     uint32_t blue_noise_size;
+    /* textures (binding 14); may be empty: every texture index then samples as white */
+    const ptgs_texture* textures;
+    uint32_t num_textures;
 } ptgs_scene_desc;
 
 typedef struct ptgs_scene_info {

@@ -243,7 +243,147 @@ typedef struct {
     int has_transparent;
     const float* bn;
     int bn_size;
+    /* global_textures[]: all levels packed RGBA8 (r | g<<8 | b<<16 | a<<24); 20 info words per texture
+     * (w0, h0, levels, srgb, level offsets); decode tables [0..255] UNORM, [256..511] sRGB */
+    uint32_t* tex_texels;
+    uint32_t* tex_info;
+    float tex_lut[512];
+    uint32_t num_tex;
 } OScene;
+
+/* ------------------------------------------------------------------------------------------ */
+/* textures: Image::createTextureImage/generateMipmaps (image.cpp:35, :203-290) and the sampler of */
+/* image.cpp:124-138 (linear/linear/linear-mip, repeat), closesthit.rchit:39-42 sampleTexture      */
+/* ------------------------------------------------------------------------------------------ */
+#define OR_TEX_INFO 20
+#define OR_TEX_MAX_LEVELS 16
+
+static float or_srgb_dec(float c) { return c <= 0.04045f ? c / 12.92f : powf((c + 0.055f) / 1.055f, 2.4f); }
+static float or_srgb_enc(float c) { return c <= 0.0031308f ? c * 12.92f : 1.055f * powf(c, 1.0f / 2.4f) - 0.055f; }
+static uint32_t or_u8(float c) {
+    float v = floorf(c * 255.0f + 0.5f);
+    if (!(v > 0.0f)) return 0u;
+    if (v > 255.0f) return 255u;
+    return (uint32_t)v;
+}
+static int or_clampi(int i, int lo, int hi) { return i < lo ? lo : (i > hi ? hi : i); }
+
+/* mip level l = linear blit of level l-1 onto max(1, w/2) x max(1, h/2): bilinear, clamp-to-edge,
+ * in linear space (sRGB decoded, filtered, re-encoded and rounded; alpha linear) */
+static int or_build_textures(OScene* s, const ptgs_texture* tex, uint32_t count) {
+    for (int i = 0; i < 256; ++i) {
+        s->tex_lut[i] = (float)i / 255.0f;
+        s->tex_lut[256 + i] = or_srgb_dec((float)i / 255.0f);
+    }
+    s->num_tex = count;
+    s->tex_info = (uint32_t*)calloc((size_t)(count ? count : 1) * OR_TEX_INFO, 4);
+    size_t total = 0;
+    for (uint32_t t = 0; t < count; ++t) {
+        uint32_t w = tex[t].width, h = tex[t].height;
+        uint32_t big = w > h ? w : h, levels = 1;
+        while ((big >> levels) > 0u) ++levels;
+        if (levels > OR_TEX_MAX_LEVELS) levels = OR_TEX_MAX_LEVELS;
+        for (uint32_t l = 0; l < levels; ++l) {
+            total += (size_t)w * h;
+            w = w > 1 ? w / 2 : 1;
+            h = h > 1 ? h / 2 : 1;
+        }
+    }
+    s->tex_texels = (uint32_t*)malloc((total ? total : 1) * 4);
+    size_t at = 0;
+    for (uint32_t t = 0; t < count; ++t) {
+        const ptgs_texture* T = &tex[t];
+        uint32_t* info = s->tex_info + (size_t)t * OR_TEX_INFO;
+        uint32_t big = T->width > T->height ? T->width : T->height, levels = 1;
+        while ((big >> levels) > 0u) ++levels;
+        if (levels > OR_TEX_MAX_LEVELS) levels = OR_TEX_MAX_LEVELS;
+        info[0] = T->width; info[1] = T->height; info[2] = levels; info[3] = T->srgb ? 1u : 0u;
+        info[4] = (uint32_t)at;
+        memcpy(s->tex_texels + at, T->rgba8, (size_t)T->width * T->height * 4);
+        at += (size_t)T->width * T->height;
+        const float* dec = s->tex_lut + (T->srgb ? 256 : 0);
+        uint32_t sw = T->width, sh = T->height;
+        for (uint32_t l = 1; l < levels; ++l) {
+            uint32_t dw = sw > 1 ? sw / 2 : 1, dh = sh > 1 ? sh / 2 : 1;
+            const uint32_t* src = s->tex_texels + info[4 + l - 1];
+            uint32_t* dst = s->tex_texels + at;
+            info[4 + l] = (uint32_t)at;
+            at += (size_t)dw * dh;
+            float sxs = (float)sw / (float)dw, sys = (float)sh / (float)dh;
+            for (uint32_t y = 0; y < dh; ++y) {
+                float fy = ((float)y + 0.5f) * sys - 0.5f, fy0 = floorf(fy), b = fy - fy0;
+                int iy = (int)fy0;
+                int y0 = or_clampi(iy, 0, (int)sh - 1), y1 = or_clampi(iy + 1, 0, (int)sh - 1);
+                for (uint32_t x = 0; x < dw; ++x) {
+                    float fx = ((float)x + 0.5f) * sxs - 0.5f, fx0 = floorf(fx), a = fx - fx0;
+                    int ix = (int)fx0;
+                    int x0 = or_clampi(ix, 0, (int)sw - 1), x1 = or_clampi(ix + 1, 0, (int)sw - 1);
+                    uint32_t q00 = src[y0 * sw + x0], q10 = src[y0 * sw + x1];
+                    uint32_t q01 = src[y1 * sw + x0], q11 = src[y1 * sw + x1];
+                    uint32_t out = 0;
+                    for (int ch = 0; ch < 4; ++ch) {
+                        const float* dd = ch == 3 ? s->tex_lut : dec;
+                        int sh8 = 8 * ch;
+                        float c00 = dd[(q00 >> sh8) & 255u], c10 = dd[(q10 >> sh8) & 255u];
+                        float c01 = dd[(q01 >> sh8) & 255u], c11 = dd[(q11 >> sh8) & 255u];
+                        float cf = (c00 * (1.0f - a) + c10 * a) * (1.0f - b) + (c01 * (1.0f - a) + c11 * a) * b;
+                        float e = (T->srgb && ch < 3) ? or_srgb_enc(cf) : cf;
+                        out |= or_u8(e) << sh8;
+                    }
+                    dst[y * dw + x] = out;
+                }
+            }
+            sw = dw; sh = dh;
+        }
+    }
+    return 0;
+}
+
+static int or_wrap(int i, int n) { int r = i % n; return r < 0 ? r + n : r; }
+
+static void or_texel(const OScene* s, uint32_t idx, uint32_t srgb, float* o) {
+    uint32_t q = s->tex_texels[idx];
+    const float* rgb = s->tex_lut + (srgb ? 256 : 0);
+    o[0] = rgb[q & 255u]; o[1] = rgb[(q >> 8) & 255u]; o[2] = rgb[(q >> 16) & 255u]; o[3] = s->tex_lut[q >> 24];
+}
+
+static void or_bilinear(const OScene* s, uint32_t base, int w, int h, uint32_t srgb, float u, float v, float* o) {
+    float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    float fx = floorf(x), fy = floorf(y), a = x - fx, b = y - fy;
+    int ix = (int)fx, iy = (int)fy;
+    int x0 = or_wrap(ix, w), x1 = or_wrap(ix + 1, w), y0 = or_wrap(iy, h), y1 = or_wrap(iy + 1, h);
+    float t00[4], t10[4], t01[4], t11[4];
+    or_texel(s, base + (uint32_t)(y0 * w + x0), srgb, t00);
+    or_texel(s, base + (uint32_t)(y0 * w + x1), srgb, t10);
+    or_texel(s, base + (uint32_t)(y1 * w + x0), srgb, t01);
+    or_texel(s, base + (uint32_t)(y1 * w + x1), srgb, t11);
+    float ia = 1.0f - a, ib = 1.0f - b;
+    for (int k = 0; k < 4; ++k) o[k] = (t00[k] * ia + t10[k] * a) * ib + (t01[k] * ia + t11[k] * a) * b;
+}
+
+/* textureLod(global_textures[id], uv, lod); id < 0 (or past the table) -> vec4(1) */
+static void or_tex_sample(const OScene* s, int id, float u, float v, float lod, float* o) {
+    if (id < 0 || (uint32_t)id >= s->num_tex) { o[0] = o[1] = o[2] = o[3] = 1.0f; return; }
+    const uint32_t* ti = s->tex_info + (uint32_t)id * OR_TEX_INFO;
+    uint32_t w0 = ti[0], h0 = ti[1], levels = ti[2], srgb = ti[3];
+    float lam = mx(lod, 0.0f), fl = floorf(lam), delta = lam - fl;
+    uint32_t dl = (uint32_t)mn(fl, (float)(levels - 1u));
+    uint32_t dh = dl + 1u < levels ? dl + 1u : dl;
+    uint32_t wl = w0 >> dl, hl = h0 >> dl;
+    or_bilinear(s, ti[4 + dl], (int)(wl ? wl : 1), (int)(hl ? hl : 1), srgb, u, v, o);
+    if (delta == 0.0f || dh == dl) return;
+    float b4[4];
+    uint32_t wh = w0 >> dh, hh = h0 >> dh;
+    or_bilinear(s, ti[4 + dh], (int)(wh ? wh : 1), (int)(hh ? hh : 1), srgb, u, v, b4);
+    float id_ = 1.0f - delta;
+    for (int k = 0; k < 4; ++k) o[k] = o[k] * id_ + b4[k] * delta;
+}
+
+static uint32_t or_tex_max_dim(const OScene* s, int id) {
+    if (id < 0 || (uint32_t)id >= s->num_tex) return 1u;
+    const uint32_t* ti = s->tex_info + (uint32_t)id * OR_TEX_INFO;
+    return ti[0] > ti[1] ? ti[0] : ti[1];
+}
 
 static float g_pad_abs;
 
@@ -337,10 +477,11 @@ static int scene_init(OScene* s, const ptgs_scene_desc* d) {
     if (g > 0) build_node(s, 0, (int)g);
     s->bn = d->blue_noise_rgba32f;
     s->bn_size = (int)d->blue_noise_size;
+    or_build_textures(s, d->textures, d->num_textures);
     return 0;
 }
 
-static void scene_free(OScene* s) { free(s->tris); free(s->nodes); }
+static void scene_free(OScene* s) { free(s->tris); free(s->nodes); free(s->tex_texels); free(s->tex_info); }
 
 /* ------------------------------------------------------------------------------------------ */
 /* traversal                                                                                   */
@@ -397,13 +538,25 @@ static float or_rnd(uint32_t* state) {
     return (float)((word >> 22u) ^ word) / 4294967296.0f;
 }
 
-/* alpha.rahit:14-61 with untextured alpha; BLEND uses a stateless (seed, triangle) hash */
-static int or_anyhit_accept(const OScene* s, const OTri* t, uint32_t seed) {
-    const ptgs_material* m = &s->d->materials[s->d->meshes[t->mesh].material_index];
+/* alpha.rahit:14-61; BLEND uses a stateless (seed, triangle) hash */
+static int or_anyhit_accept(const OScene* s, const OTri* t, float u, float v, uint32_t seed) {
+    const ptgs_mesh_info* info = &s->d->meshes[t->mesh];
+    const ptgs_material* m = &s->d->materials[info->material_index];
     float cutoff = m->alpha_cutoff;
     int blend = m->pad > 0.5f;
     if (cutoff == 0.0f && !blend) return 1;
     float alpha = m->base_color_factor[3];
+    if (m->albedo_texture_index > 0) {
+        const ptgs_vertex* vs = s->d->vertices + info->vertex_offset;
+        const uint32_t* ix = s->d->indices + info->index_offset + t->prim * 3u;
+        const ptgs_vertex *v0 = &vs[ix[0]], *v1 = &vs[ix[1]], *v2 = &vs[ix[2]];
+        float bx = (1.0f - u) - v;
+        float tu = (v0->tex_coord[0] * bx + v1->tex_coord[0] * u) + v2->tex_coord[0] * v;
+        float tv = (v0->tex_coord[1] * bx + v1->tex_coord[1] * u) + v2->tex_coord[1] * v;
+        float o[4];
+        or_tex_sample(s, m->albedo_texture_index, tu, tv, 0.0f, o);
+        alpha = alpha * o[3];
+    }
     if (cutoff > 0.0f) return !(alpha < cutoff);
     uint32_t h = seed ^ (t->gid * 0x9E3779B9u);
     return !(or_rnd(&h) > alpha);
@@ -419,7 +572,7 @@ static void closest(const OScene* s, const ONode* n, const ORay* r, OHit* h, uin
             if (!tri_intersect(r, t, &tt, &u, &v)) continue;
             if (!(tt >= r->tmin && tt <= h->t)) continue;
             if (tt == h->t && t->gid >= h->gid) continue;
-            if (s->has_transparent && (t->flags & 1u) && !or_anyhit_accept(s, t, seed)) continue;
+            if (s->has_transparent && (t->flags & 1u) && !or_anyhit_accept(s, t, u, v, seed)) continue;
             h->t = tt; h->u = u; h->v = v; h->gid = t->gid; h->tri = t;
         }
         return;
@@ -436,7 +589,7 @@ static int anyhit(const OScene* s, const ONode* n, const ORay* r, uint32_t seed)
             float tt, u, v;
             if (!tri_intersect(r, t, &tt, &u, &v)) continue;
             if (!(tt >= r->tmin && tt <= r->tmax)) continue;
-            if (s->has_transparent && (t->flags & 1u) && !or_anyhit_accept(s, t, seed)) continue;
+            if (s->has_transparent && (t->flags & 1u) && !or_anyhit_accept(s, t, u, v, seed)) continue;
             return 1;
         }
         return 0;
@@ -469,7 +622,7 @@ typedef struct {
     float inv_view[16], inv_proj[16];
     float ambient[4];
     float emissive_flux, punctual_flux, p_emissive;
-    float lod_factor;
+    float lod_factor, fov, win_height, use_lod;
 } OCam;
 
 typedef struct {
@@ -692,28 +845,108 @@ static void or_closest_hit(OCtx* c, OPayload* p, const ORay* ray, const OHit* hi
     v3 ng_orig = ng;
     if (dot(ng, vv) < 0.0f) ng = neg(ng);
     v3 N = ng;
-    (void)tw; (void)tg;  /* tangent frame only feeds the normal map (textures: not supported) */
+    const OScene* sc = c->s;
+    float tcu = (v0->tex_coord[0] * bx + v1->tex_coord[0] * by) + v2->tex_coord[0] * bz;
+    float tcv = (v0->tex_coord[1] * bx + v1->tex_coord[1] * by) + v2->tex_coord[1] * bz;
+    v3 T = tg;
+    int tvalid = (fabsf(tw) > 0.001f) && (len(T) > 0.001f);
+    if (!tvalid) {
+        v3 up = (fabsf(N.y) < 0.999f) ? V(0.0f, 1.0f, 0.0f) : V(1.0f, 0.0f, 0.0f);
+        T = safe_nrm(cross(up, N));
+    }
+    /* :358-385 normal map */
+    if (fabsf(tw) > 0.0001f && mat->normal_texture_index > 0) {
+        float hand = (tw < 0.0f) ? -1.0f : 1.0f;
+        v3 B = mul(safe_nrm(cross(N, T)), hand);
+        float tex_lod = 0.0f;
+        if (cp->use_lod > 0.0f) {
+            if (p->last_pdf <= 0.0f) {
+                if (mat->albedo_texture_index > 0) { /* computeLOD :21-37 */
+                    float sn, cs;
+                    or_sincos(cp->fov * 0.5f, &sn, &cs);
+                    float spread = (2.0f * (sn / cs)) / cp->win_height;
+                    float fp = hit->t * spread;
+                    float ndv = fabsf(dot(ng, neg(ray->d)));
+                    fp = fp / mx(ndv, 0.25f);
+                    float dim = (float)or_tex_max_dim(sc, mat->albedo_texture_index);
+                    float raw = or_log2(fp * dim);
+                    float bias = (dim > 2048.0f) ? 0.0f : -0.5f;
+                    tex_lod = mx(raw * 0.7f + bias, 0.0f);
+                }
+            } else {
+                tex_lod = clampf_(mat->roughness_factor * 5.0f + or_log2(hit->t * 0.1f + 1.0f), 0.0f, 8.0f);
+            }
+        }
+        const float* un = mat->uv_normal;
+        float nu = ((un[0] * tcu + un[4] * tcv) + un[8] * 0.0f) + un[12];
+        float nv = ((un[1] * tcu + un[5] * tcv) + un[9] * 0.0f) + un[13];
+        float m4[4];
+        or_tex_sample(sc, mat->normal_texture_index, nu, nv, tex_lod, m4);
+        v3 nm = V(m4[0] * 2.0f - 1.0f, m4[1] * 2.0f - 1.0f, m4[2] * 2.0f - 1.0f);
+        nm.x = nm.x * cp->lod_factor;
+        nm.y = nm.y * cp->lod_factor;
+        nm = nrm(nm);
+        N = safe_nrm(add(add(mul(T, nm.x), mul(B, nm.y)), mul(N, nm.z)));
+    }
 
     union { float f; int32_t i; } pun;
     pun.f = mat->use_specular_glossiness_workflow;
     int32_t sgb = pun.i;
     v3 bcf = ld3(mat->base_color_factor);
+    v3 bcs = S(1.0f);
+    if (mat->albedo_texture_index > 0) {
+        float b4[4];
+        or_tex_sample(sc, mat->albedo_texture_index, tcu, tcv, 0.0f, b4);
+        bcs = V(b4[0], b4[1], b4[2]);
+    }
     v3 albedo, f0;
     float rough, metal;
     if ((float)sgb > 0.5f) {
-        albedo = mulv(bcf, vcol);
-        f0 = ld3(mat->specular_color_factor);
-        rough = sqrtf(mx(1.0f - mat->roughness_factor, 0.04f));
+        albedo = mulv(mulv(bcf, vcol), bcs);
+        v3 spec = ld3(mat->specular_color_factor);
+        float gloss = mat->roughness_factor;
+        if (mat->sg_id > 0) {
+            float g4[4];
+            or_tex_sample(sc, mat->sg_id, tcu, tcv, 0.0f, g4);
+            spec = mulv(spec, V(g4[0], g4[1], g4[2]));
+            gloss = gloss * g4[3];
+        }
+        f0 = spec;
+        rough = sqrtf(mx(1.0f - gloss, 0.04f));
         metal = 0.0f;
     } else {
-        albedo = mulv(bcf, vcol);
+        albedo = mulv(mulv(bcf, vcol), bcs);
         metal = mat->metallic_factor;
         rough = mat->roughness_factor;
+        if (mat->metallic_roughness_texture_index > 0) {
+            float r4[4];
+            or_tex_sample(sc, mat->metallic_roughness_texture_index, tcu, tcv, 0.0f, r4);
+            metal = metal * r4[2];
+            rough = rough * r4[1];
+        }
         f0 = mix3_(S(0.04f), albedo, metal);
         albedo = mul(albedo, 1.0f - metal);
     }
     float cc = mat->clearcoat_factor, ccr = mat->clearcoat_roughness_factor;
+    if (cc > 0.0f && mat->clearcoat_texture_index > 0) {
+        float q[4];
+        or_tex_sample(sc, mat->clearcoat_texture_index, tcu, tcv, 0.0f, q);
+        cc = cc * q[0];
+    }
+    if (cc > 0.0f && mat->clearcoat_roughness_texture_index > 0) {
+        float q[4];
+        or_tex_sample(sc, mat->clearcoat_roughness_texture_index, tcu, tcv, 0.0f, q);
+        ccr = ccr * q[0];
+    }
     v3 em = ld3(mat->emissive_factor_and_pad);
+    if (len(em) > 0.0f && mat->emissive_texture_index > 0) {
+        const float* ue = mat->uv_emissive;
+        float eu = ((ue[0] * tcu + ue[4] * tcv) + ue[8] * 0.0f) + ue[12];
+        float ev = ((ue[1] * tcu + ue[5] * tcv) + ue[9] * 0.0f) + ue[13];
+        float q[4];
+        or_tex_sample(sc, mat->emissive_texture_index, eu, ev, 0.0f, q);
+        em = mulv(em, V(q[0], q[1], q[2]));
+    }
     float tr = mat->transmission_factor;
     if (with_hitpos) { p->hit_pos = hp; p->normal = N; }
 
@@ -936,6 +1169,9 @@ static void fill_cam(OCam* c, const ptgs_ubo* ubo) {
     c->punctual_flux = ubo->punctual_flux;
     c->p_emissive = ubo->p_emissive;
     c->lod_factor = ubo->lod_factor;
+    c->fov = ubo->fov;
+    c->win_height = ubo->height;
+    c->use_lod = ubo->use_lod;
 }
 
 /* ------------------------------------------------------------------------------------------ */

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptgs.so")
 
@@ -88,7 +88,12 @@ class SceneDesc(C.Structure):
                 ("light_triangles", C.c_void_p), ("num_light_triangles", C.c_uint32), ("light_cdf", C.c_void_p),
                 ("num_light_cdf", C.c_uint32), ("punctual_lights", C.c_void_p), ("num_punctual_lights", C.c_uint32),
                 ("punctual_cdf", C.c_void_p), ("num_punctual_cdf", C.c_uint32), ("blue_noise_rgba32f", C.c_void_p),
-                ("blue_noise_size", C.c_uint32)]
+                ("blue_noise_size", C.c_uint32), ("textures", C.c_void_p), ("num_textures", C.c_uint32)]
+
+
+class Texture(C.Structure):
+    _fields_ = [("rgba8", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32), ("srgb", C.c_uint32),
+                ("reserved", C.c_uint32)]
 
 
 class SceneInfo(C.Structure):

@@ -21,6 +21,7 @@
 #include "hostmath.h"
 #include "pt_launch.h"
 #include "splat.h"
+#include "textures.h"
 
 using namespace ptgs;
 
@@ -143,6 +144,13 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
   uint32_t bn = d->blue_noise_size;
   if (!d->blue_noise_rgba32f || bn == 0 || (bn & (bn - 1)) != 0)
     return fail(c, PTGS_EINVAL, "blue noise must be a power-of-two square RGBA32F texture");
+  if (d->num_textures && !d->textures) return fail(c, PTGS_EINVAL, "textures is null");
+  TexturePool texpool;
+  {
+    std::string terr;
+    if (!build_texture_pool(d->textures, d->num_textures, texpool, terr)) return fail(c, PTGS_EINVAL, "%s", terr.c_str());
+    if (texpool.texels.size() >= (1ull << 32)) return fail(c, PTGS_ERANGE, "texture pool exceeds 2^32 texels");
+  }
 
   // gather triangles in flattening order (gid), skipping meshes with < 3 indices (engine.cpp:545-547)
   std::vector<BuildTri> tris;
@@ -208,6 +216,18 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
   if ((rc = upload(c, d->punctual_lights, d->num_punctual_lights, &s.plights))) return rc;
   if ((rc = upload(c, d->punctual_cdf, d->num_punctual_cdf, &s.pcdf))) return rc;
   if ((rc = upload(c, (const float4*)d->blue_noise_rgba32f, (size_t)bn * bn, &s.blue_noise))) return rc;
+  if ((rc = upload(c, texpool.texels.data(), texpool.texels.size(), &s.tex.texels))) return rc;
+  if ((rc = upload(c, texpool.info.data(), texpool.info.size(), &s.tex.info))) return rc;
+  if ((rc = upload(c, texpool.lut.data(), texpool.lut.size(), &s.tex.lut))) return rc;
+  s.tex.count = d->num_textures;
+  s.uses_textures = 0;
+  for (uint32_t i = 0; i < d->num_materials; ++i) {
+    const ptgs_material& m = d->materials[i];
+    if (m.albedo_texture_index > 0 || m.normal_texture_index > 0 || m.metallic_roughness_texture_index > 0 ||
+        m.emissive_texture_index > 0 || m.clearcoat_texture_index > 0 || m.clearcoat_roughness_texture_index > 0 ||
+        m.sg_id > 0)
+      s.uses_textures = 1;
+  }
   s.num_light_cdf = d->num_light_cdf;
   s.num_plights = d->num_punctual_lights;
   s.bn_size = (int32_t)bn;

@@ -14,6 +14,7 @@
 
 #include <hip/hip_runtime.h>
 #include "detmath.h"
+#include "texture.h"
 #include "../../include/ptgs/ptgs.h"
 
 namespace ptgs {
@@ -36,6 +37,8 @@ struct DevScene {
   const ptgs_punctual_light* plights;
   const ptgs_punctual_cdf* pcdf;
   const float4* blue_noise;
+  DevTextures tex;                // global_textures[] (texture.h)
+  int32_t uses_textures;          // some material has a texture index > 0: launch the TEX kernels
   uint32_t num_light_cdf;
   uint32_t num_plights;
   int32_t bn_size;
@@ -167,12 +170,29 @@ __device__ __forceinline__ bool tri_isect(const Ray& r, v3 v0, v3 e1, v3 e2, flo
 // ---------------------------------------------------------------------------------------------
 // Materials / any-hit (alpha.rahit:14-61, untextured alpha = base_color_factor.a)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool anyhit_accept(const DevScene& sc, uint32_t mesh, uint32_t seed, uint32_t gid) {
-  const ptgs_material& m = sc.materials[sc.meshes[mesh].material_index];
+// TEX = false: no material of the scene references a texture (scene flag), the texture branch is
+// compiled out (it costs the path-tracer kernel registers even when never taken)
+template <bool TEX>
+__device__ __forceinline__ bool anyhit_accept(const DevScene& sc, uint32_t mesh, uint32_t prim, float u, float v,
+                                              uint32_t seed, uint32_t gid) {
+  const ptgs_mesh_info info = sc.meshes[mesh];
+  const ptgs_material& m = sc.materials[info.material_index];
   float alpha_cutoff = m.alpha_cutoff;
   bool is_blend = m.pad > 0.5f;
   if (alpha_cutoff == 0.0f && !is_blend) return true;
   float alpha = m.base_color_factor[3];
+  if (TEX && m.albedo_texture_index > 0) {  // alpha.rahit:28-45: interpolated UV, LOD 0
+    const uint32_t i0 = sc.indices[info.index_offset + prim * 3u + 0u];
+    const uint32_t i1 = sc.indices[info.index_offset + prim * 3u + 1u];
+    const uint32_t i2 = sc.indices[info.index_offset + prim * 3u + 2u];
+    const ptgs_vertex& v0 = sc.vertices[info.vertex_offset + i0];
+    const ptgs_vertex& v1 = sc.vertices[info.vertex_offset + i1];
+    const ptgs_vertex& v2 = sc.vertices[info.vertex_offset + i2];
+    const float bx = (1.0f - u) - v;
+    const float tu = (v0.tex_coord[0] * bx + v1.tex_coord[0] * u) + v2.tex_coord[0] * v;
+    const float tv = (v0.tex_coord[1] * bx + v1.tex_coord[1] * u) + v2.tex_coord[1] * v;
+    alpha = alpha * sample_texture(sc.tex, m.albedo_texture_index, tu, tv, 0.0f).w;
+  }
   if (alpha_cutoff > 0.0f) return !(alpha < alpha_cutoff);
   return !(alpha_hash(seed, gid) > alpha);
 }
@@ -180,7 +200,7 @@ __device__ __forceinline__ bool anyhit_accept(const DevScene& sc, uint32_t mesh,
 // ---------------------------------------------------------------------------------------------
 // Traversal
 // ---------------------------------------------------------------------------------------------
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, int leaf, Hit& h,
                                              uint32_t seed, TraversalCounters& cnt) {
   uint32_t L = (uint32_t)(~leaf);
@@ -196,13 +216,13 @@ __device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, i
     uint32_t gid = f2u(c.w);
     if (t == h.t && gid >= h.gid) continue;
     if (sc.has_transparent && (sc.tri_flags[start + k] & 1u)) {
-      if (!anyhit_accept(sc, f2u(a.w), seed, gid)) continue;
+      if (!anyhit_accept<TEX>(sc, f2u(a.w), f2u(b.w), u, v, seed, gid)) continue;
     }
     h.t = t; h.u = u; h.v = v; h.gid = gid; h.slot = start + k;
   }
 }
 
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
                                              TraversalCounters& cnt) {
   Hit h; h.t = r.tmax; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu; h.slot = 0;
@@ -230,14 +250,14 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
         node = stack[(--sp) * PTGS_BLOCK];
       }
     }
-    leaf_closest<STATS>(sc, r, node, h, seed, cnt);
+    leaf_closest<STATS, TEX>(sc, r, node, h, seed, cnt);
     if (sp == 0) return h;
     node = stack[(--sp) * PTGS_BLOCK];
   }
 }
 
 // any-hit: true if something blocks the segment [tmin, tmax]
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
                                           TraversalCounters& cnt) {
   int sp = 0;
@@ -275,7 +295,7 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
       if (!tri_isect(r, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), t, u, v)) continue;
       if (!(t >= r.tmin && t <= r.tmax)) continue;
       if (sc.has_transparent && (sc.tri_flags[start + k] & 1u)) {
-        if (!anyhit_accept(sc, f2u(a.w), seed, f2u(c.w))) continue;
+        if (!anyhit_accept<TEX>(sc, f2u(a.w), f2u(b.w), u, v, seed, f2u(c.w))) continue;
       }
       return true;
     }
@@ -392,20 +412,20 @@ __device__ __forceinline__ float pdf_ggx(v3 n, v3 v, v3 l, float roughness) {
 // :109-111
 __device__ __forceinline__ float pdf_lambert(v3 n, v3 l) { return fmaxx(dot3(n, l), 0.0f) / PT_PI; }
 
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ __forceinline__ float trace_shadow_dist(ShadeCtx& c, v3 o, v3 d, float maxd, uint32_t seed, TraversalCounters& cnt) {
   c.shadow_rays++;
   Ray r = make_ray(o, d, 0.001f, maxd);
-  return trace_any<STATS>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
+  return trace_any<STATS, TEX>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
 }
 
 // :119-126
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ __forceinline__ float trace_shadow(ShadeCtx& c, v3 o, v3 light_pos, uint32_t seed, TraversalCounters& cnt) {
   v3 l = light_pos - o;
   float dist = length3(l);
   l = safe_normalize(l);
-  return trace_shadow_dist<STATS>(c, o, l, dist - 0.005f, seed, cnt);
+  return trace_shadow_dist<STATS, TEX>(c, o, l, dist - 0.005f, seed, cnt);
 }
 
 // binary search over a CDF (closesthit.rchit:131-137 / :197-203 / :262-268)
@@ -421,7 +441,7 @@ __device__ __forceinline__ uint32_t cdf_search(const CDF* cdf, uint32_t n, float
 }
 
 // :128-192
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ void sample_punctual(ShadeCtx& c, const Payload& p, v3 hit_pos, v3 n, v3 n_geo, v3 v, v3 albedo,
                                 float roughness, v3 f0, float transmission, v3& lo, TraversalCounters& cnt) {
   const DevScene& sc = *c.sc;
@@ -461,8 +481,8 @@ __device__ void sample_punctual(ShadeCtx& c, const Payload& p, v3 hit_pos, v3 n,
   if (ndl > 0.0f && length3(le) > 0.0f) {
     v3 so = hit_pos + n_geo * 0.001f;
     float vis;
-    if (light.type == 1) vis = trace_shadow_dist<STATS>(c, so, l, 10000.0f, p.seed, cnt);
-    else vis = trace_shadow<STATS>(c, so, lpos, p.seed, cnt);
+    if (light.type == 1) vis = trace_shadow_dist<STATS, TEX>(c, so, l, 10000.0f, p.seed, cnt);
+    else vis = trace_shadow<STATS, TEX>(c, so, lpos, p.seed, cnt);
     vis = fmaxx(vis, transmission);
     if (vis > 0.0f) {
       float weight = (float)num_lights;
@@ -479,7 +499,7 @@ __device__ void sample_punctual(ShadeCtx& c, const Payload& p, v3 hit_pos, v3 n,
 }
 
 // :194-257 (sg == true) and :259-320 (sg == false)
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ void sample_emissive(ShadeCtx& c, const Payload& p, bool sg, v3 hit_pos, v3 n, v3 n_geo, v3 v,
                                 v3 albedo, float roughness, float metallic, v3 f0, float transmission, v3& lo,
                                 TraversalCounters& cnt) {
@@ -508,7 +528,7 @@ __device__ void sample_emissive(ShadeCtx& c, const Payload& p, bool sg, v3 hit_p
   float ldn = absx(dot3(-l, ln));
   if (ndl > 0.0f && ldn > 0.0f) {
     v3 so = hit_pos + n_geo * 0.001f;
-    float vis = trace_shadow<STATS>(c, so, lp, p.seed, cnt);
+    float vis = trace_shadow<STATS, TEX>(c, so, lp, p.seed, cnt);
     vis = fmaxx(vis, transmission);
     if (vis > 0.0f) {
       const ptgs_material& lm = sc.materials[tri.material_index];

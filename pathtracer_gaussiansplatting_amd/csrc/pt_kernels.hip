@@ -61,7 +61,7 @@ __device__ __forceinline__ float4 blue_noise_texel(const DevScene& sc, uint32_t 
 #define PTGS_PT_MIN_WAVES 4
 #endif
 
-template <bool STATS>
+template <bool STATS, bool TEX>
 __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevScene sc, CamParams cp, float4* __restrict__ accum,
                                                         uint32_t W, uint32_t H, uint32_t row0, uint32_t row1,
                                                         uint32_t spp, uint32_t frame0, uint32_t stride,
@@ -114,10 +114,10 @@ __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevSc
         p.depth = depth;
         Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
         ext_rays++;
-        Hit h = trace_closest<STATS>(sc, ray, p.seed, c.stack, tc);
+        Hit h = trace_closest<STATS, TEX>(sc, ray, p.seed, c.stack, tc);
         if (STATS && h.gid != 0xffffffffu) tc.hits++;
         if (h.gid == 0xffffffffu) miss<false>(cp, p);
-        else closest_hit<STATS, false>(c, p, ray, h, tc);
+        else closest_hit<STATS, false, TEX>(c, p, ray, h, tc);
         acc = acc + p.color * thr;
         acc = vmin(acc, 5.0f);
         if (p.hit_flag < 0.0f) break;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevSc
   flush_counters(counters, ext_rays, c.shadow_rays, samples, tc, STATS);
 }
 
-template <bool STATS>
+template <bool STATS, bool TEX>
 __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp, TorusParams tp,
                                                        const ptgs_ray_sample* __restrict__ samples,
                                                        uint32_t n, uint32_t side, uint32_t frame,
@@ -193,10 +193,10 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
 
     Ray ray = make_ray(so, rd, 0.0f, 10000.0f);
     ext_rays++;
-    Hit h = trace_closest<STATS>(sc, ray, p.seed, c.stack, tc);
+    Hit h = trace_closest<STATS, TEX>(sc, ray, p.seed, c.stack, tc);
     if (STATS && h.gid != 0xffffffffu) tc.hits++;
     if (h.gid == 0xffffffffu) miss<true>(cp, p);
-    else closest_hit<STATS, true>(c, p, ray, h, tc);
+    else closest_hit<STATS, true, TEX>(c, p, ray, h, tc);
 
     v3 fpos = p.hit_pos;
     float fflag = p.hit_flag;
@@ -215,10 +215,10 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
         }
         Ray r2 = make_ray(p.next_o, p.next_d, 0.001f, 10000.0f);
         ext_rays++;
-        Hit h2 = trace_closest<STATS>(sc, r2, p.seed, c.stack, tc);
+        Hit h2 = trace_closest<STATS, TEX>(sc, r2, p.seed, c.stack, tc);
         if (STATS && h2.gid != 0xffffffffu) tc.hits++;
         if (h2.gid == 0xffffffffu) miss<true>(cp, p);
-        else closest_hit<STATS, true>(c, p, r2, h2, tc);
+        else closest_hit<STATS, true, TEX>(c, p, r2, h2, tc);
         acc = acc + p.color * thr;
         acc = vmin(acc, 5.0f);
         if (p.hit_flag < 1.5f) break;
@@ -250,12 +250,11 @@ hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accu
   if (row1 <= row0 || spp == 0) return hipSuccess;
   dim3 grid((W + 15u) / 16u, (row1 - row0 + 15u) / 16u);
   dim3 block(256);
-  if (stats)
-    hipLaunchKernelGGL(pt_camera_kernel<true>, grid, block, 0, stream, sc, cp, (float4*)accum, W, H, row0, row1,
-                       spp, frame0, stride, mode, counters);
-  else
-    hipLaunchKernelGGL(pt_camera_kernel<false>, grid, block, 0, stream, sc, cp, (float4*)accum, W, H, row0, row1,
-                       spp, frame0, stride, mode, counters);
+  // (STATS, TEX) instantiations: TEX only for scenes whose materials reference textures
+  auto k = stats ? (sc.uses_textures ? pt_camera_kernel<true, true> : pt_camera_kernel<true, false>)
+                 : (sc.uses_textures ? pt_camera_kernel<false, true> : pt_camera_kernel<false, false>);
+  hipLaunchKernelGGL(k, grid, block, 0, stream, sc, cp, (float4*)accum, W, H, row0, row1, spp, frame0, stride, mode,
+                     counters);
   return hipGetLastError();
 }
 
@@ -265,10 +264,9 @@ hipError_t launch_pt_torus(const DevScene& sc, const CamParams& cp, const TorusP
   if (n == 0) return hipSuccess;
   dim3 grid((n + 255u) / 256u);
   dim3 block(256);
-  if (stats)
-    hipLaunchKernelGGL(pt_torus_kernel<true>, grid, block, 0, stream, sc, cp, tp, samples, n, side, frame, hits, counters);
-  else
-    hipLaunchKernelGGL(pt_torus_kernel<false>, grid, block, 0, stream, sc, cp, tp, samples, n, side, frame, hits, counters);
+  auto k = stats ? (sc.uses_textures ? pt_torus_kernel<true, true> : pt_torus_kernel<true, false>)
+                 : (sc.uses_textures ? pt_torus_kernel<false, true> : pt_torus_kernel<false, false>);
+  hipLaunchKernelGGL(k, grid, block, 0, stream, sc, cp, tp, samples, n, side, frame, hits, counters);
   return hipGetLastError();
 }
 

@@ -1,15 +1,28 @@
 // pt_shade.h — closest-hit shading, restating shaders/rt_render/closesthit.rchit:324-621
 // (WITH_HITPOS = the rt_datacollect variant, which also writes payload.hit_pos / normal,
-// shaders/rt_datacollect/closesthit.rchit:443-447). Textures are not sampled yet: every
-// sampleTexture() behind an "id > 0" guard returns vec4(1) (untextured scenes are exact; see
-// DESIGN.md "textures").
+// shaders/rt_datacollect/closesthit.rchit:443-447). Textures: texture.h (sampleTexture :39-42,
+// computeLOD :21-37).
 #pragma once
 
 #include "pt_device.h"
 
 namespace ptgs {
 
-template <bool STATS, bool WITH_HITPOS>
+// closesthit.rchit:21-37 computeLOD (the ray origin argument is unused there)
+__device__ __forceinline__ float compute_lod(const CamParams& cp, const DevTextures& tx, v3 dir, float dist, v3 normal,
+                                             int tex_id) {
+  const float spread = (2.0f * tanx(cp.fov * 0.5f)) / cp.win_height;
+  float footprint = dist * spread;
+  const float ndv = absx(dot3(normal, -dir));
+  footprint = footprint / fmaxx(ndv, 0.25f);
+  float dim = 2048.0f;
+  if (tex_id >= 0) dim = (float)texture_max_dim(tx, tex_id);
+  const float raw = log2x(footprint * dim);
+  const float bias = (dim > 2048.0f) ? 0.0f : -0.5f;
+  return fmaxx(raw * 0.7f + bias, 0.0f);
+}
+
+template <bool STATS, bool WITH_HITPOS, bool TEX>
 __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& hit, TraversalCounters& cnt) {
   const DevScene& sc = *c.sc;
   const CamParams& cp = *c.cp;
@@ -30,6 +43,8 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
   // :336-346
   float bx = (1.0f - hit.u) - hit.v, by = hit.u, bz = hit.v;
   v3 hit_pos = ray.o + ray.d * hit.t;
+  const float tc_u = (v0.tex_coord[0] * bx + v1.tex_coord[0] * by) + v2.tex_coord[0] * bz;
+  const float tc_v = (v0.tex_coord[1] * bx + v1.tex_coord[1] * by) + v2.tex_coord[1] * bz;
   v3 vcol = (ld3(v0.color) * bx + ld3(v1.color) * by) + ld3(v2.color) * bz;
   v3 nobj = (ld3(v0.normal) * bx + ld3(v1.normal) * by) + ld3(v2.normal) * bz;
   v3 tobj = (ld3(v0.tangent) * bx + ld3(v1.tangent) * by) + ld3(v2.tangent) * bz;
@@ -38,7 +53,6 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
   v3 n_geo = safe_normalize(nobj);
   v3 t_geo = safe_normalize(tobj);
   t_geo = safe_normalize(t_geo - n_geo * dot3(t_geo, n_geo));
-  (void)t_geo;
 
   v3 V = -ray.d;
   v3 n_geo_orig = n_geo;
@@ -50,9 +64,29 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
     v3 up = (absx(N.y) < 0.999f) ? mk3(0.f, 1.f, 0.f) : mk3(1.f, 0.f, 0.f);
     T = safe_normalize(cross3(up, N));
   }
-  // Normal map (:364-385) needs textures, which are not uploaded yet: the block is skipped, so
-  // N stays the flipped geometric normal (exact for scenes without normal_id > 0).
-  (void)T;
+  // :358-385 tangent frame + normal map
+  if (TEX && absx(tw) > 0.0001f && mat.normal_texture_index > 0) {
+    const float handed = (tw < 0.0f) ? -1.0f : 1.0f;
+    const v3 B = safe_normalize(cross3(N, T)) * handed;
+    float tex_lod = 0.0f;
+    if (cp.use_lod > 0.0f) {
+      if (p.last_pdf <= 0.0f) {
+        if (mat.albedo_texture_index > 0)
+          tex_lod = compute_lod(cp, sc.tex, ray.d, hit.t, n_geo, mat.albedo_texture_index);
+      } else {
+        tex_lod = clampf(mat.roughness_factor * 5.0f + log2x(hit.t * 0.1f + 1.0f), 0.0f, 8.0f);
+      }
+    }
+    const float* un = mat.uv_normal;  // (uv_normal * vec4(tc, 0, 1)).xy
+    const float nu = ((un[0] * tc_u + un[4] * tc_v) + un[8] * 0.0f) + un[12];
+    const float nv = ((un[1] * tc_u + un[5] * tc_v) + un[9] * 0.0f) + un[13];
+    const v4 mv = sample_texture(sc.tex, mat.normal_texture_index, nu, nv, tex_lod);
+    v3 nm = mk3(mv.x * 2.0f - 1.0f, mv.y * 2.0f - 1.0f, mv.z * 2.0f - 1.0f);
+    nm.x = nm.x * cp.lod_factor;
+    nm.y = nm.y * cp.lod_factor;
+    nm = normalize3(nm);
+    N = safe_normalize((T * nm.x + B * nm.y) + N * nm.z);
+  }
 
   v3 albedo, f0;
   float roughness, metallic;
@@ -61,24 +95,51 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
     union { float f; int32_t i; } pun; pun.f = mat.use_specular_glossiness_workflow;
     sg_bits = pun.i;  // float stored, int read
   }
+  v3 bcs = mk3(1.0f);  // :393-394 base colour sample
+  if (TEX && mat.albedo_texture_index > 0) {
+    const v4 b4 = sample_texture(sc.tex, mat.albedo_texture_index, tc_u, tc_v, 0.0f);
+    bcs = mk3(b4.x, b4.y, b4.z);
+  }
   v3 bcf = mk3(mat.base_color_factor[0], mat.base_color_factor[1], mat.base_color_factor[2]);
   if ((float)sg_bits > 0.5f) {
-    albedo = bcf * vcol;  // * base_color_sample (1)
+    albedo = (bcf * vcol) * bcs;
     v3 spec_col = ld3(mat.specular_color_factor);
     float gloss = mat.roughness_factor;
+    if (TEX && mat.sg_id > 0) {
+      const v4 sg4 = sample_texture(sc.tex, mat.sg_id, tc_u, tc_v, 0.0f);
+      spec_col = spec_col * mk3(sg4.x, sg4.y, sg4.z);
+      gloss = gloss * sg4.w;
+    }
     f0 = spec_col;
     roughness = sqrtx(fmaxx(1.0f - gloss, 0.04f));
     metallic = 0.0f;
   } else {
-    albedo = bcf * vcol;
+    albedo = (bcf * vcol) * bcs;
     metallic = mat.metallic_factor;
     roughness = mat.roughness_factor;
+    if (TEX && mat.metallic_roughness_texture_index > 0) {
+      const v4 mr = sample_texture(sc.tex, mat.metallic_roughness_texture_index, tc_u, tc_v, 0.0f);
+      metallic = metallic * mr.z;
+      roughness = roughness * mr.y;
+    }
     f0 = mix3(mk3(0.04f), albedo, metallic);
     albedo = albedo * (1.0f - metallic);
   }
   float clearcoat = mat.clearcoat_factor;
   float cc_rough = mat.clearcoat_roughness_factor;
+  if (TEX && clearcoat > 0.0f && mat.clearcoat_texture_index > 0)
+    clearcoat = clearcoat * sample_texture(sc.tex, mat.clearcoat_texture_index, tc_u, tc_v, 0.0f).x;
+  if (TEX && clearcoat > 0.0f && mat.clearcoat_roughness_texture_index > 0)
+    cc_rough = cc_rough * sample_texture(sc.tex, mat.clearcoat_roughness_texture_index, tc_u, tc_v, 0.0f).x;
+  // (:432-434 occlusion is fetched but never used by the reference: not restated)
   v3 emissive = ld3(mat.emissive_factor_and_pad);
+  if (TEX && length3(emissive) > 0.0f && mat.emissive_texture_index > 0) {  // :437-440
+    const float* ue = mat.uv_emissive;
+    const float eu = ((ue[0] * tc_u + ue[4] * tc_v) + ue[8] * 0.0f) + ue[12];
+    const float ev = ((ue[1] * tc_u + ue[5] * tc_v) + ue[9] * 0.0f) + ue[13];
+    const v4 e4 = sample_texture(sc.tex, mat.emissive_texture_index, eu, ev, 0.0f);
+    emissive = emissive * mk3(e4.x, e4.y, e4.z);
+  }
   float transmission = mat.transmission_factor;
 
   if (WITH_HITPOS) {
@@ -122,18 +183,18 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
     float p_punctual = 1.0f - cp.p_emissive;
     if (blue_noise_dim(p, 10) < cp.p_emissive) {
       if (use_nee) {
-        sample_emissive<STATS>(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, lc, cnt);
+        sample_emissive<STATS, TEX>(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, lc, cnt);
         lc = lc * (1.0f / cp.p_emissive);
       }
     } else {
-      sample_punctual<STATS>(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, lc, cnt);
+      sample_punctual<STATS, TEX>(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, lc, cnt);
       lc = lc * (1.0f / p_punctual);
     }
     lo = lo + lc;
   } else if (has_emissive && use_nee) {
-    sample_emissive<STATS>(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, lo, cnt);
+    sample_emissive<STATS, TEX>(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, lo, cnt);
   } else if (has_punctual) {
-    sample_punctual<STATS>(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, lo, cnt);
+    sample_punctual<STATS, TEX>(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, lo, cnt);
   }
   p.color = lo;
 

@@ -94,6 +94,9 @@ class Scene:
     total_flux: float
     p_emissive: float
     blue_noise: np.ndarray | None = None  # (S, S, 4) float32
+    # global_textures[]: (rgba8 (H, W, 4) uint8, srgb) pairs; material texture indices index this list
+    # (index 0 is the reference's default white texture, gameobject.cpp:347-349)
+    textures: list = field(default_factory=list)
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -120,6 +123,15 @@ class Scene:
         d.punctual_lights, d.num_punctual_lights = pl.ctypes.data, len(pl)
         d.punctual_cdf, d.num_punctual_cdf = pc.ctypes.data, len(pc)
         d.blue_noise_rgba32f, d.blue_noise_size = bn.ctypes.data, bn.shape[0]
+        if self.textures:
+            pix = [np.ascontiguousarray(t[0], np.uint8) for t in self.textures]
+            tex = (_abi.Texture * len(pix))()
+            for k, (img, (_, srgb)) in enumerate(zip(pix, self.textures)):
+                if img.ndim != 3 or img.shape[2] != 4:
+                    raise ValueError(f"texture {k}: expected (H, W, 4) uint8, got {img.shape}")
+                tex[k].rgba8, tex[k].height, tex[k].width, tex[k].srgb = img.ctypes.data, img.shape[0], img.shape[1], int(bool(srgb))
+            self._keep += pix + [tex]
+            d.textures, d.num_textures = C.cast(tex, C.c_void_p), len(pix)
         return d
 
 

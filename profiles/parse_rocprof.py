@@ -75,7 +75,7 @@ def main(tag, workload):
         wa = sum(w) / len(w) if w else float("nan")
         hbm = (2 * fa + wa) * 1024
         lines.append(f"| {name[:90]} | {vg} | {fa:.1f} | {wa:.1f} | {hbm:.4g} |")
-        if "pt_camera_kernel<false>" in name:
+        if "pt_camera_kernel<false" in name:
             traffic.setdefault("candidates", []).append({"name": name, "vgpr": vg, "hbm": hbm,
                                                          "fetch_kib": fa, "write_kib": wa})
     # the timed (non-instrumented) pt kernel is the <false> instantiation (profile.sh keeps full names)

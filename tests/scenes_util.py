@@ -48,7 +48,45 @@ def _mat(**kw):
     return m
 
 
-def features(with_punctual=True, transparent=True):
+def _tex_rgba(h, w, seed, lo=0, hi=256):
+    rng = np.random.default_rng(seed)
+    return rng.integers(lo, hi, (h, w, 4), dtype=np.int64).astype(np.uint8)
+
+
+def feature_textures():
+    """global_textures[] for features(textured=True): sizes and formats chosen to cover odd mip chains,
+    both formats, repeat wrapping (UVs outside [0, 1]) and texture alpha."""
+    yy, xx = np.mgrid[0:64, 0:48]
+    checker = ((yy // 8 + xx // 8) % 2).astype(np.float64)
+    albedo = np.zeros((64, 48, 4), np.uint8)
+    albedo[..., 0] = 60 + 180 * checker
+    albedo[..., 1] = 40 + 120 * (xx / 47.0)
+    albedo[..., 2] = 200 - 150 * checker
+    albedo[..., 3] = np.where((yy // 4) % 3 == 0, 40, 230)  # alpha stripes for BLEND / MASK
+    ny, nx = np.mgrid[0:32, 0:32] * (2 * np.pi / 32)
+    n = np.stack([0.5 * np.sin(nx), 0.5 * np.cos(ny), np.ones_like(nx)], -1)
+    n /= np.linalg.norm(n, axis=-1, keepdims=True)
+    nmap = np.zeros((32, 32, 4), np.uint8)
+    nmap[..., :3] = np.round((n * 0.5 + 0.5) * 255)
+    nmap[..., 3] = 255
+    return [
+        (np.full((1, 1, 4), 255, np.uint8), True),  # 0: default white (gameobject.cpp:347-349)
+        (albedo, True),                             # 1: base colour (sRGB) with alpha
+        (nmap, False),                              # 2: normal map (UNORM)
+        (_tex_rgba(16, 16, 3), False),              # 3: metal-rough (UNORM: g rough, b metal)
+        (_tex_rgba(8, 8, 4, 64), True),             # 4: emissive (sRGB)
+        (_tex_rgba(16, 16, 5), True),               # 5: spec-gloss (sRGB: rgb spec, a gloss)
+        (_tex_rgba(16, 16, 6), False),              # 6: clearcoat (UNORM r)
+        (_tex_rgba(3, 5, 7), True),                 # 7: odd 5x3 base colour (mip chain 5x3 -> 2x1 -> 1x1)
+        (_tex_rgba(9, 7, 8), False),                # 8: clearcoat roughness (UNORM r)
+    ]
+
+
+def _planar_uv(pos):
+    return np.stack([pos[:, 0] * 0.7 + pos[:, 2] * 0.3, pos[:, 1] * 0.9 - pos[:, 2] * 0.4], -1)
+
+
+def features(with_punctual=True, transparent=True, textured=False):
     objs = []
     # (mesh, material)
     objs.append((Y._box([-2.0, 1.0, -1.5], [0.8, 1.0, 0.8]), _mat(transmission_factor=1.0, metallic_factor=0.0,
@@ -69,13 +107,32 @@ def features(with_punctual=True, transparent=True):
                                                                    metallic_factor=0.0)))
         objs.append((Y._box([-0.5, 3.2, -0.5], [0.4, 0.1, 0.4]),
                      _mat(pad=1.0, alpha_cutoff=0.5, base_color_factor=[1.0, 0.2, 0.2, 0.3], metallic_factor=0.0)))
+    tex_ids = []
+    if textured:  # global indices into feature_textures(), set on the flattened materials below
+        tex_ids = [dict(normal_texture_index=2),
+                   dict(albedo_texture_index=1, normal_texture_index=2, clearcoat_texture_index=6,
+                        clearcoat_roughness_texture_index=8),
+                   dict(albedo_texture_index=7, metallic_roughness_texture_index=3),
+                   dict(albedo_texture_index=1, sg_id=5),
+                   dict(emissive_texture_index=4),
+                   dict(albedo_texture_index=1),
+                   dict(albedo_texture_index=1)]
+        uvn = np.eye(4, dtype=np.float32)
+        uvn[0, 0], uvn[1, 1], uvn[3, 0], uvn[3, 1] = 1.5, 0.75, 0.25, -0.5  # column-major: m[12], m[13]
+        objs[1][1]["uv_normal"] = uvn.reshape(-1)
+        uve = np.eye(4, dtype=np.float32)
+        uve[0, 0], uve[3, 1] = 2.0, 0.3
+        objs[4][1]["uv_emissive"] = uve.reshape(-1)
     b = S.SceneBuilder()
-    for (pos, nrm, tri), m in objs:
+    for k, ((pos, nrm, tri), m) in enumerate(objs):
         v = np.zeros(len(pos), VERTEX_DTYPE)
         v["pos"] = pos
         v["normal"] = nrm
         v["color"] = 1.0
         v["tangent"] = [1.0, 0.0, 0.0, 0.0]
+        if textured:
+            v["tex_coord"] = _planar_uv(np.asarray(pos, np.float32))
+            v["tangent"] = [0.0, 0.0, 1.0, -1.0 if k % 2 else 1.0]
         idx = tri.reshape(-1).astype(np.uint32)
         prims = np.zeros(1, PRIMITIVE_DTYPE)
         prims["index_count"] = len(idx)
@@ -106,6 +163,16 @@ def features(with_punctual=True, transparent=True):
     b.add_rtbox_json(os.path.join(S.SCENES_DIR, "cornell_box.json"))
     sc = b.finalize()
     sc.blue_noise = blue_noise()
+    if textured:
+        sc.textures = feature_textures()
+        tex_fields = ("albedo_texture_index", "normal_texture_index", "metallic_roughness_texture_index",
+                      "emissive_texture_index", "occlusion_texture_index", "clearcoat_texture_index",
+                      "clearcoat_roughness_texture_index", "sg_id")
+        for key in tex_fields:  # the builder offset every object's default texture: one shared table here
+            sc.materials[key] = 0
+        for k, ids in enumerate(tex_ids):  # one material per object, in object order
+            for key, val in ids.items():
+                sc.materials[k][key] = val
     return sc
 
 

@@ -33,7 +33,7 @@ def test_every_declared_symbol_is_exported(native_lib):
 
 
 def test_abi_version_and_arch(native_lib):
-    assert native_lib.ptgs_abi_version() == 1
+    assert native_lib.ptgs_abi_version() == 2
     assert native_lib.ptgs_device_arch() == b"gfx950"
 
 
@@ -56,6 +56,10 @@ def test_struct_layouts():
     assert _abi.HITDATA_DTYPE.itemsize == 48 and _abi.HITDATA_DTYPE.fields["flag"][1] == 12
     assert _abi.HITDATA_DTYPE.fields["normal"][1] == 32
     assert C.sizeof(_abi.RayPush) == 80 and _abi.RayPush.mode.offset == 64 and _abi.RayPush.height.offset == 76
+    # ptgs.h (ABI 2): ptgs_texture and the texture table at the end of ptgs_scene_desc
+    assert C.sizeof(_abi.Texture) == 24 and _abi.Texture.srgb.offset == 16
+    assert _abi.SceneDesc.textures.offset == _abi.SceneDesc.blue_noise_size.offset + 8
+    assert _abi.SceneDesc.num_textures.offset == _abi.SceneDesc.textures.offset + 8
 
 
 def test_compute_path_fails_loudly_without_gpu(native_lib):

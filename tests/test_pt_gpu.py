@@ -77,6 +77,25 @@ def test_features_all_branches(renderer, oracle_lib):
     print(f"features rel L2 {err:.2e}, {nd} pixels differ")
 
 
+@pytest.mark.parametrize("use_lod", [0.0, 1.0])
+def test_features_textured(renderer, oracle_lib, use_lod):
+    """closesthit.rchit texture paths: base colour / spec-gloss / metal-rough / clearcoat (+ roughness) /
+    emissive (uv_emissive) samples, tangent-space normal map (uv_normal, lod_factor, computeLOD with
+    use_lod), texture alpha in any-hit, odd mip chains, repeat wrapping."""
+    sc = U.features(textured=True)
+    ubo = make_ubo(U.cornell_pose(160 / 120), sc, 0, ambient=(0.05, 0.05, 0.08, 1.0))
+    ubo.use_lod = use_lod
+    ubo.lod_factor = 0.8
+    g, sg = _gpu_render(renderer, sc, ubo, 160, 120, 3)
+    o, so = _oracle_render(oracle_lib, sc, ubo, 160, 120, 3)
+    err, nd = _compare(g, o, sg, so)
+    print(f"textured (use_lod {use_lod}) rel L2 {err:.2e}, {nd} pixels differ")
+    plain = U.features()
+    o2, _ = _oracle_render(oracle_lib, plain, make_ubo(U.cornell_pose(160 / 120), plain, 0,
+                                                        ambient=(0.05, 0.05, 0.08, 1.0)), 160, 120, 3)
+    assert U.rel_l2(o, o2) > 1e-2  # the textures change the image
+
+
 def test_atrium_250k(renderer, oracle_lib):
     """C3 scene (250k triangles, sun + emissive panel) at a reduced resolution."""
     sc = U.atrium()
