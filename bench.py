@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gs", action="store_true")
     ap.add_argument("--no-pt", action="store_true")
+    ap.add_argument("--no-hybrid", action="store_true")
+    ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
+    ap.add_argument("--hybrid-spp", type=int, default=16)
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented counting pass")
     return ap.parse_args()
 
@@ -240,6 +243,49 @@ def main():
         if args.no_pt:
             out.update({"value": out["gs"]["value"], "unit": "Gsplats/s", "ms_per_step": out["gs"]["ms_per_step"],
                         "config": {"workload": out["gs"]["workload"]}, "data": "synthetic Gaussians (seeded)"})
+
+    # ------------------------------------------------------------------ hybrid (C4), one GPU
+    # C2-distributed Gaussians (seed 3) placed in the C3 camera's frame + the C3 mesh: path trace
+    # (hybrid_spp), primary-hit depth, splat over the traced frame (build-defined).
+    if not args.no_pt and not args.no_hybrid and world == 1:
+        hg = Y.gaussians_c2(args.hybrid_gaussians, seed=3)
+        hubo0 = make_ubo(pose, scene, 0, ambient=(0.3, 0.4, 0.5, 1.0), height=H)
+        view = np.array(hubo0.view, np.float64).reshape(4, 4).T  # column-major -> row-major
+        inv = np.linalg.inv(view)
+        m = np.concatenate([hg["means"].astype(np.float64), np.ones((len(hg["means"]), 1))], 1)
+        hg["means"] = (m @ inv.T)[:, :3].astype(np.float32)
+        hdg = {k: torch.from_numpy(v).cuda() for k, v in hg.items()}
+        haccum = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        hdepth = torch.zeros((H, W), dtype=torch.float32, device="cuda")
+        hframe = 0
+
+        def hybrid_step():
+            nonlocal hframe
+            hubo = make_ubo(pose, scene, hframe, ambient=(0.3, 0.4, 0.5, 1.0), height=H)
+            r.trace_camera(hubo, W, H, haccum, spp=args.hybrid_spp, stream=stream)
+            r.trace_depth(hubo, W, H, hdepth, stream=stream)
+            r.splat_gaussians(hdg, hubo, W, H, haccum, over=(hdepth, haccum), stream=stream)
+            hframe += args.hybrid_spp
+
+        for _ in range(max(args.warmup, 1)):
+            hybrid_step()
+        torch.cuda.synchronize()
+        r.stats_reset(stream)
+        hsteps = max(args.steps, 3)
+        t0 = time.perf_counter()
+        for _ in range(hsteps):
+            hybrid_step()
+        torch.cuda.synchronize()
+        hdt = (time.perf_counter() - t0) / hsteps
+        hst = r.stats()
+        out["hybrid"] = {
+            "workload": f"C4 hybrid: {args.hybrid_gaussians} C2-distributed Gaussians + the C3 mesh, {W}x{H}, "
+                        f"{args.hybrid_spp} spp path trace + primary-hit depth + splat-over composite",
+            "frames_per_s": round(1.0 / hdt, 3), "ms_per_frame": round(hdt * 1e3, 3),
+            "mrays_per_s": round((hst.extension_rays + hst.shadow_rays) / hsteps / hdt / 1e6, 2),
+            "gsplats_per_s": round(args.hybrid_gaussians / hdt / 1e9, 4),
+        }
+        del haccum, hdepth, hdg
 
     # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_pt:

@@ -256,6 +256,13 @@ int ptgs_trace_camera_rows(ptgs_ctx* ctx, const ptgs_ubo* ubo, uint32_t width, u
                            uint32_t row_begin, uint32_t row_end, float* accum_rgba32f, uint32_t spp,
                            uint32_t frame_stride, uint32_t accum_mode, void* hip_stream);
 
+/* Primary-hit depth for compositing (hybrid C4): per pixel the camera ray of
+ * raygen_camera.rgen:25-41 through the pixel centre (no jitter), closest hit (any-hit seed from
+ * ubo->frame_count), view-space depth -(view * hit).z; +inf where the ray misses. depth: device
+ * float[W*H]. */
+int ptgs_trace_depth(ptgs_ctx* ctx, const ptgs_ubo* ubo, uint32_t width, uint32_t height, float* depth,
+                     void* hip_stream);
+
 /* Toroidal data-collection tracer (shaders/rt_datacollect/raygen.rgen:31-141): one ray per
  * RaySample (device array, n entries), launch grid side x side with side = ceil(sqrt(n))
  * (engine.cpp:2786), HitData running mean written in place (device array, n entries). */
@@ -319,6 +326,16 @@ int ptgs_splat_gaussians(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo*
                          uint32_t tile_row_begin, uint32_t tile_row_end, float* out_rgba32f,
                          ptgs_splat_stats* stats, void* hip_stream);
 
+/* Hybrid composite (C4): the same splat, front to back over an image: a pixel stops at the first
+ * Gaussian whose view depth is >= depth[pixel] (the mesh occludes it and everything behind), and
+ * out = C + T * under (all four channels, C.a = 1 - T). depth: device float[W*H] (e.g. from
+ * ptgs_trace_depth); under: device RGBA32F[W*H] (e.g. the ptgs_trace_camera accumulator); out may
+ * alias under. Integer outputs (keys, values, ranges) are those of ptgs_splat_gaussians. */
+int ptgs_splat_gaussians_over(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t width,
+                              uint32_t height, const float* depth, const float* under_rgba32f,
+                              uint32_t tile_row_begin, uint32_t tile_row_end, float* out_rgba32f,
+                              ptgs_splat_stats* stats, void* hip_stream);
+
 /* Debug/parity access to the integer intermediates of the most recent ptgs_splat_gaussians call
  * (device buffers owned by the context, valid until the next splat call):
  * radii[N] (int32), tiles_touched[N] (u32), sorted keys[K] (u64: tile<<32 | depth bits),
@@ -339,8 +356,8 @@ typedef struct ptgs_splat_buffers {
 int ptgs_splat_get_buffers(const ptgs_ctx* ctx, ptgs_splat_buffers* out);
 
 /* With PTGS_FLAG_TIME_STAGES: milliseconds of the stages of the most recent ptgs_splat_gaussians
- * call, measured with hipEvents on its stream: [0] preprocess [1] scan [2] duplicate [3] sort
- * [4] ranges [5] blend. Synchronises. */
+ * call, measured with hipEvents on its stream: [0] preprocess [1] count (tile histograms, K)
+ * [2] scatter (pairs into tile segments) [3] 0 [4] 0 [5] sort + blend. Synchronises. */
 int ptgs_splat_stage_ms(ptgs_ctx* ctx, float out_ms[6]);
 
 /* ---------------- output encode (blit rgba32f -> B8G8R8A8_SRGB, engine.cpp:2004-2020) --------- */

@@ -53,7 +53,9 @@ def lib() -> C.CDLL:
         L.oracle_splat_points.restype = None
         L.oracle_splat_points.argtypes = [_P, _P, _P, _P, _U, _U, _U, _P, _P]
         L.oracle_splat_gaussians.restype = C.c_int
-        L.oracle_splat_gaussians.argtypes = [_P, _P, _P, _P, _P, _U, _P, _U, _U, _P, _U, _U, _P, _P, _P, _P, _P,
+        L.oracle_trace_depth.restype = C.c_int
+        L.oracle_trace_depth.argtypes = [_P, _P, _U, _U, _P, C.c_int]
+        L.oracle_splat_gaussians.argtypes = [_P, _P, _P, _P, _P, _U, _P, _U, _U, _P, _P, _P, _U, _U, _P, _P, _P, _P, _P,
                                              C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)), _P,
                                              _P]
         L.oracle_free.restype = None
@@ -116,7 +118,15 @@ def splat_points(ubo, push, hits, samples, width, height, rgba8: np.ndarray, dep
                               len(hits), width, height, rgba8.ctypes.data, depth.ctypes.data)
 
 
-def splat_gaussians(g: dict, ubo, width, height, bg=(0.0, 0.0, 0.0), tile_rows=None):
+def trace_depth(desc, ubo, width, height, threads=0) -> np.ndarray:
+    """Primary-hit view depth per pixel ((H, W) float32, +inf on a miss)."""
+    out = np.zeros((height, width), np.float32)
+    lib().oracle_trace_depth(C.byref(desc), C.byref(ubo), width, height, out.ctypes.data, threads)
+    return out
+
+
+def splat_gaussians(g: dict, ubo, width, height, bg=(0.0, 0.0, 0.0), tile_rows=None, over=None):
+    """over=(depth (H, W) float32, under (H, W, 4) float32): the hybrid composite."""
     n = g["means"].shape[0]
     arrs = {k: np.ascontiguousarray(v, np.float32) for k, v in g.items()}
     radii = np.zeros(n, np.int32)
@@ -131,9 +141,14 @@ def splat_gaussians(g: dict, ubo, width, height, bg=(0.0, 0.0, 0.0), tile_rows=N
     kp = C.POINTER(C.c_uint64)()
     vp = C.POINTER(C.c_uint32)()
     t0, t1 = (0, 0xFFFFFFFF) if tile_rows is None else tile_rows
+    dl = un = None
+    if over is not None:
+        dl = np.ascontiguousarray(over[0], np.float32)
+        un = np.ascontiguousarray(over[1], np.float32)
     K = lib().oracle_splat_gaussians(arrs["means"].ctypes.data, arrs["scales"].ctypes.data,
                                      arrs["rotations"].ctypes.data, arrs["opacities"].ctypes.data,
                                      arrs["colors"].ctypes.data, n, C.addressof(ubo), width, height, bgc.ctypes.data,
+                                     None if dl is None else dl.ctypes.data, None if un is None else un.ctypes.data,
                                      t0, t1, radii.ctypes.data, touched.ctypes.data, means2d.ctypes.data,
                                      depths.ctypes.data, conic.ctypes.data, C.byref(kp), C.byref(vp),
                                      ranges.ctypes.data, image.ctypes.data)

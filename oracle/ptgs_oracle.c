@@ -1413,11 +1413,56 @@ static int ndc_rect(float v, int r, int blk, int grid, int hi) {
 
 /* Outputs (caller-allocated): radii[N], touched[N], means2d[2N], depths[N], conic[4N]. Returns K and
  * allocates keys_out / vals_out (malloc; caller frees) sorted by (key, gaussian); ranges[tiles*2]; image. */
+/* primary-hit view depth (the product's ptgs_trace_depth): pixel-centre camera ray of
+ * raygen_camera.rgen:25-41, closest hit with the frame's any-hit seed, -(view * hit).z, +inf on a miss */
+int oracle_trace_depth(const ptgs_scene_desc* d, const ptgs_ubo* ubo, uint32_t W, uint32_t H, float* depth,
+                       int threads) {
+    OScene s;
+    scene_init(&s, d);
+    OCam cam;
+    fill_cam(&cam, ubo);
+    long long total = (long long)W * H;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 256)
+#endif
+    for (long long k = 0; k < total; ++k) {
+        uint32_t x = (uint32_t)(k % W), y = (uint32_t)(k / W);
+        uint32_t seed = y * W + x + ubo->frame_count * 719393u;
+        float ux = ((float)x + 0.5f) / (float)W, uy = ((float)y + 0.5f) / (float)H;
+        float dx = ux * 2.0f - 1.0f, dy = uy * 2.0f - 1.0f;
+        float o4[4], t4[4], d4[4];
+        float e0[4] = {0.f, 0.f, 0.f, 1.f};
+        mv(cam.inv_view, e0, o4);
+        float tv[4] = {dx, dy, 1.f, 1.f};
+        mv(cam.inv_proj, tv, t4);
+        v3 dc = nrm(divs(V(t4[0], t4[1], t4[2]), t4[3]));
+        float dv[4] = {dc.x, dc.y, dc.z, 0.f};
+        mv(cam.inv_view, dv, d4);
+        v3 ro = V(o4[0], o4[1], o4[2]);
+        v3 rd = nrm(V(d4[0], d4[1], d4[2]));
+        ORay r = mkray(ro, rd, 0.001f, 10000.0f);
+        OHit h = trace_closest(&s, &r, seed);
+        float out = INFINITY;
+        if (h.tri) {
+            v3 hp = add(ro, mul(rd, h.t));
+            float hv[4] = {hp.x, hp.y, hp.z, 1.0f}, pv[4];
+            mv(ubo->view, hv, pv);
+            out = -pv[2];
+        }
+        depth[k] = out;
+    }
+    scene_free(&s);
+    return 0;
+}
+
+/* depth / under (both NULL, or W*H arrays): the hybrid composite of ptgs_splat_gaussians_over — a
+ * pixel stops at the first Gaussian with depth >= depth[pixel]; out = C + T * under */
 int oracle_splat_gaussians(const float* means, const float* scales, const float* rots, const float* opac,
                            const float* colors, uint32_t n, const ptgs_ubo* ubo, uint32_t W, uint32_t H,
-                           const float* bg, uint32_t trow0, uint32_t trow1, int32_t* radii, uint32_t* touched,
-                           float* means2d, float* depths, float* conic, uint64_t** keys_out, uint32_t** vals_out,
-                           uint32_t* ranges, float* image) {
+                           const float* bg, const float* depth_lim, const float* under, uint32_t trow0, uint32_t trow1,
+                           int32_t* radii, uint32_t* touched, float* means2d, float* depths, float* conic,
+                           uint64_t** keys_out, uint32_t** vals_out, uint32_t* ranges, float* image) {
     const int BX = 16, BY = 16;
     float mvp[16];
     mm(ubo->proj, ubo->view, mvp);
@@ -1531,8 +1576,10 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
                     uint32_t px = tx * BX + lx, py = ty * BY + ly;
                     if (px >= W || py >= H) continue;
                     float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+                    size_t pix = (size_t)py * W + px;
                     for (uint32_t j = s0; j < s1; ++j) {
                         uint32_t g = vals[j];
+                        if (depth_lim && !(depths[g] < depth_lim[pix])) break;
                         float dx = means2d[2 * g] - (float)px, dy = means2d[2 * g + 1] - (float)py;
                         const float* co = conic + 4 * g;
                         float power = -0.5f * ((co[0] * dx) * dx + (co[2] * dy) * dy) - (co[1] * dx) * dy;
@@ -1546,11 +1593,19 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
                         C2 = C2 + (colors[3 * g + 2] * alpha) * T;
                         T = test_T;
                     }
-                    float* o = image + 4 * ((size_t)py * W + px);
-                    o[0] = C0 + T * bg[0];
-                    o[1] = C1 + T * bg[1];
-                    o[2] = C2 + T * bg[2];
-                    o[3] = 1.0f - T;
+                    float* o = image + 4 * pix;
+                    if (under) {
+                        const float* u = under + 4 * pix;
+                        o[0] = C0 + T * u[0];
+                        o[1] = C1 + T * u[1];
+                        o[2] = C2 + T * u[2];
+                        o[3] = (1.0f - T) + T * u[3];
+                    } else {
+                        o[0] = C0 + T * bg[0];
+                        o[1] = C1 + T * bg[1];
+                        o[2] = C2 + T * bg[2];
+                        o[3] = 1.0f - T;
+                    }
                 }
         }
     *keys_out = keys;

@@ -142,12 +142,15 @@ SYMBOLS = {
     "ptgs_trace_camera": (_I, [_P, C.POINTER(Ubo), _U, _U, _P, _U, _U, _U, _P]),
     "ptgs_trace_camera_rows": (_I, [_P, C.POINTER(Ubo), _U, _U, _U, _U, _P, _U, _U, _U, _P]),
     "ptgs_trace_torus": (_I, [_P, C.POINTER(Ubo), C.POINTER(RayPush), _P, _U, _P, _P]),
+    "ptgs_trace_depth": (_I, [_P, C.POINTER(Ubo), _U, _U, _P, _P]),
     "ptgs_set_flags": (_I, [_P, _U]),
     "ptgs_stats_reset": (_I, [_P, _P]),
     "ptgs_stats_read": (_I, [_P, C.POINTER(TraceStats)]),
     "ptgs_splat_points": (_I, [_P, C.POINTER(Ubo), C.POINTER(RayPush), _P, _P, _U, _U, _U, _P, _P, _P]),
     "ptgs_splat_gaussians": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _FP, _U, _U, _P,
                                   C.POINTER(SplatStats), _P]),
+    "ptgs_splat_gaussians_over": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _P, _P, _U, _U, _P,
+                                       C.POINTER(SplatStats), _P]),
     "ptgs_splat_get_buffers": (_I, [_P, C.POINTER(SplatBuffers)]),
     "ptgs_splat_stage_ms": (_I, [_P, _FP]),
     "ptgs_encode_srgb8": (_I, [_P, _P, _U, _U, _P, _P]),

@@ -276,6 +276,22 @@ int ptgs_trace_camera(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_t h, 
   return ptgs_trace_camera_rows(c, ubo, w, h, 0, h, accum, spp, frame_stride, accum_mode, stream);
 }
 
+int ptgs_trace_depth(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_t h, float* depth, void* stream) {
+  if (!c || !ubo || !depth) return fail(c, PTGS_EINVAL, "null argument");
+  if (!c->has_scene) return fail(c, PTGS_ENOSCENE, "no scene uploaded");
+  if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
+  if (!is_device_ptr(depth)) return fail(c, PTGS_EINVAL, "depth is not a device pointer");
+  HIPCHK(c, hipSetDevice(c->device));
+  CamParams cp;
+  int rc = fill_cam(c, ubo, cp);
+  if (rc) return rc;
+  ViewMat vm;
+  std::memcpy(vm.m, ubo->view, sizeof(vm.m));
+  hipError_t e = launch_pt_depth(c->dsc, cp, vm, depth, w, h, ubo->frame_count, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "pt_depth launch: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
 int ptgs_trace_torus(ptgs_ctx* c, const ptgs_ubo* ubo, const ptgs_ray_push* push, const ptgs_ray_sample* samples,
                      uint32_t n, ptgs_hitdata* hits, void* stream) {
   if (!c || !ubo || !push) return fail(c, PTGS_EINVAL, "null argument");
@@ -369,24 +385,40 @@ int ptgs_synchronize(ptgs_ctx* c) {
 
 extern "C" {
 
-int ptgs_splat_gaussians(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
-                         const float bg[3], uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
-                         ptgs_splat_stats* stats, void* stream) {
-  if (!c || !g || !ubo || !out || !bg) return fail(c, PTGS_EINVAL, "null argument");
+static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
+                        const float bg[3], const float* depth, const float* under, uint32_t tile_row_begin,
+                        uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream) {
   if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
   if (g->count && (!is_device_ptr(g->means) || !is_device_ptr(g->scales) || !is_device_ptr(g->rotations) ||
                    !is_device_ptr(g->opacities) || !is_device_ptr(g->colors)))
     return fail(c, PTGS_EINVAL, "gaussian arrays must be device pointers");
   if (!is_device_ptr(out)) return fail(c, PTGS_EINVAL, "out is not a device pointer");
+  if ((depth && !is_device_ptr(depth)) || (under && !is_device_ptr(under)))
+    return fail(c, PTGS_EINVAL, "depth / under must be device pointers");
   if (ubo->proj[0] == 0.0f || ubo->proj[5] == 0.0f) return fail(c, PTGS_EINVAL, "degenerate projection");
   HIPCHK(c, hipSetDevice(c->device));
   float mvp[16];
   mat4_mul(ubo->proj, ubo->view, mvp);
-  hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, tile_row_begin,
-                                 tile_row_end, out, stats, (c->flags & PTGS_FLAG_TIME_STAGES) != 0,
+  hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, depth, under,
+                                 tile_row_begin, tile_row_end, out, stats, (c->flags & PTGS_FLAG_TIME_STAGES) != 0,
                                  (hipStream_t)stream);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_gaussians: %s", hipGetErrorString(e));
   return PTGS_OK;
+}
+
+int ptgs_splat_gaussians(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
+                         const float bg[3], uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
+                         ptgs_splat_stats* stats, void* stream) {
+  if (!c || !g || !ubo || !out || !bg) return fail(c, PTGS_EINVAL, "null argument");
+  return splat_common(c, g, ubo, w, h, bg, nullptr, nullptr, tile_row_begin, tile_row_end, out, stats, stream);
+}
+
+int ptgs_splat_gaussians_over(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
+                              const float* depth, const float* under_rgba32f, uint32_t tile_row_begin,
+                              uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream) {
+  if (!c || !g || !ubo || !out || !depth || !under_rgba32f) return fail(c, PTGS_EINVAL, "null argument");
+  const float zero[3] = {0.0f, 0.0f, 0.0f};
+  return splat_common(c, g, ubo, w, h, zero, depth, under_rgba32f, tile_row_begin, tile_row_end, out, stats, stream);
 }
 
 int ptgs_splat_get_buffers(const ptgs_ctx* c, ptgs_splat_buffers* out) {

@@ -4,6 +4,8 @@
 //                      `spp` consecutive samples per launch; the running mean of :80-87 is kept in
 //                      registers across samples, which is bit-identical to one RMW per frame).
 //   pt_torus_kernel  : shaders/rt_datacollect/raygen.rgen:31-141 (one work-item per RaySample).
+//   pt_depth_kernel  : primary-hit view depth per pixel (pixel-centre ray of raygen_camera.rgen:25-41)
+//                      for the hybrid splat-over-path-trace composite.
 //
 // Launch geometry: 256-thread workgroups = 4 waves, each wave an 8x8 pixel tile (primary-ray
 // coherence for the BVH walk), workgroup = 16x16 pixels; 1080p -> 8,160 workgroups (>> 256 CUs).
@@ -241,6 +243,39 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
   flush_counters(counters, ext_rays, c.shadow_rays, nsamp, tc, STATS);
 }
 
+// Primary-hit depth: the camera ray of raygen_camera.rgen:25-41 through the pixel centre (no
+// jitter), closest hit with the frame's any-hit seed (index + frame_count * 719393, :21); depth =
+// view-space distance -(view * hit).z of the hit point, +inf on a miss. One work-item per pixel.
+template <bool TEX>
+__global__ __launch_bounds__(256) void pt_depth_kernel(DevScene sc, CamParams cp, ViewMat vm, float* __restrict__ depth,
+                                                       uint32_t W, uint32_t H, uint32_t frame) {
+  const uint32_t lid = threadIdx.x;
+  const uint32_t wave = lid >> 6, lane = lid & 63u;
+  const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+  const uint32_t y = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+  __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
+  if (x >= W || y >= H) return;
+  TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
+  const uint32_t seed = y * W + x + frame * 719393u;
+  const float ux = ((float)x + 0.5f) / (float)W, uy = ((float)y + 0.5f) / (float)H;
+  const float dx = ux * 2.0f - 1.0f, dy = uy * 2.0f - 1.0f;
+  const v4 origin = matvec(cp.inv_view, mk4(0.f, 0.f, 0.f, 1.f));
+  const v4 target = matvec(cp.inv_proj, mk4(dx, dy, 1.f, 1.f));
+  const v3 dirc = normalize3(mk3(target.x, target.y, target.z) / target.w);
+  const v4 direction = matvec(cp.inv_view, mk4(dirc.x, dirc.y, dirc.z, 0.f));
+  const v3 ro = mk3(origin.x, origin.y, origin.z);
+  const v3 rd = normalize3(mk3(direction.x, direction.y, direction.z));
+  const Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
+  const Hit h = trace_closest<false, TEX>(sc, ray, seed, s_stack + threadIdx.x, tc);
+  float d = __builtin_huge_valf();
+  if (h.gid != 0xffffffffu) {
+    const v3 hp = ro + rd * h.t;
+    const v4 pv = matvec(vm.m, mk4(hp.x, hp.y, hp.z, 1.0f));
+    d = -pv.z;
+  }
+  depth[(size_t)y * W + x] = d;
+}
+
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
@@ -255,6 +290,14 @@ hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accu
                  : (sc.uses_textures ? pt_camera_kernel<false, true> : pt_camera_kernel<false, false>);
   hipLaunchKernelGGL(k, grid, block, 0, stream, sc, cp, (float4*)accum, W, H, row0, row1, spp, frame0, stride, mode,
                      counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_pt_depth(const DevScene& sc, const CamParams& cp, const ViewMat& vm, float* depth, uint32_t W,
+                           uint32_t H, uint32_t frame, hipStream_t stream) {
+  dim3 grid((W + 15u) / 16u, (H + 15u) / 16u);
+  auto k = sc.uses_textures ? pt_depth_kernel<true> : pt_depth_kernel<false>;
+  hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, sc, cp, vm, depth, W, H, frame);
   return hipGetLastError();
 }
 

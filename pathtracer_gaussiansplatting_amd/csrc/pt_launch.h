@@ -12,6 +12,13 @@ struct TorusParams {
   float major_radius, minor_radius, height;
 };
 
+struct ViewMat {  // ubo.view (column-major)
+  float m[16];
+};
+
+hipError_t launch_pt_depth(const DevScene& sc, const CamParams& cp, const ViewMat& vm, float* depth, uint32_t W,
+                           uint32_t H, uint32_t frame, hipStream_t stream);
+
 hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accum, uint32_t W, uint32_t H,
                             uint32_t row0, uint32_t row1, uint32_t spp, uint32_t frame0, uint32_t stride,
                             uint32_t mode, unsigned long long* counters, bool stats, hipStream_t stream);

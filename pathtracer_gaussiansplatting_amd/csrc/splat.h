@@ -13,10 +13,11 @@ SplatWorkspace* splat_workspace_create();
 void splat_workspace_destroy(SplatWorkspace* w);
 
 // view/mvp column-major float[16]; p00 = proj[0][0], p11 = proj[1][1] (negative: Vulkan y-down)
+// depth / under (both null, or both device arrays of W*H): the hybrid "over" composite
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
-                           float p11, uint32_t W, uint32_t H, const float bg[3], uint32_t tile_row_begin,
-                           uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, bool time_stages,
-                           hipStream_t s);
+                           float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
+                           const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
+                           ptgs_splat_stats* stats, bool time_stages, hipStream_t s);
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
 void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out);
 hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long** keys);

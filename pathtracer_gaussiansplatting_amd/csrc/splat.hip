@@ -197,7 +197,7 @@ __device__ __forceinline__ void gs_preprocess_one(const SplatCam& cam, const Pre
   rects[i] = make_ushort4((unsigned short)rmin_x, (unsigned short)rmin_y, (unsigned short)rmax_x,
                           (unsigned short)rmax_y);
   // Blend record (3 x float4), the form the blend loop consumes:
-  //   (x, y, A, B), (C, log2 o, r, g), (b, ex, ey, 0)  with  A = -a/2 log2e, B = -b log2e, C = -c/2 log2e
+  //   (x, y, A, B), (C, log2 o, r, g), (b, ex, ey, depth)  with  A = -a/2 log2e, B = -b log2e, C = -c/2 log2e
   // so that z = A dx^2 + B dx dy + C dy^2 + log2 o = power * log2e + log2 o and alpha = min(0.99, 2^z).
   // (ex, ey): half-extents of the ellipse where alpha >= 1/255 can hold (power >= -ln(255 o), minus a
   // 1e-3 margin, +1% and +0.01 px): the blend skips whole 8x8 pixel blocks outside that box.
@@ -208,7 +208,7 @@ __device__ __forceinline__ void gs_preprocess_one(const SplatCam& cam, const Pre
   const float ey = sq > 0.0f ? sqrtx(sq * cc) * 1.01f + 0.01f : -1.0f;
   rec[3 * i] = make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E);
   rec[3 * i + 1] = make_float4(-0.5f * con.z * L2E, __log2f(con.w), colors[3 * i], colors[3 * i + 1]);
-  rec[3 * i + 2] = make_float4(colors[3 * i + 2], ex, ey, 0.0f);
+  rec[3 * i + 2] = make_float4(colors[3 * i + 2], ex, ey, d);
 }
 
 __global__ __launch_bounds__(256) void gs_preprocess_kernel(SplatCam cam, PreArgs A) {
@@ -452,6 +452,8 @@ struct GStage {  // one staged blend record (see gs_preprocess_kernel)
 //           the Gaussians that can touch its 64 pixels. alpha = min(0.99, 2^z) with the hardware exp2
 //           (within 1e-4 relative L2 of the oracle's exp, test_raster_gpu.py); front to back, stop
 //           before the Gaussian that would take T below 1e-4 (the reference's rule).
+// OVER (hybrid composite): per-pixel depth limit and an "under" image instead of the background colour
+template <bool OVER>
 __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, const uint2* __restrict__ ranges,
                                                                  unsigned long long* __restrict__ pairs,
                                                                  unsigned long long* __restrict__ keys_out,
@@ -461,6 +463,8 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
                                                                  const uint32_t* __restrict__ total, uint32_t cap,
                                                                  uint32_t slot_keys,
                                                                  const unsigned long long* __restrict__ tile_slots,
+                                                                 const float* __restrict__ depth_lim,
+                                                                 const float4* __restrict__ under,
                                                                  float4* __restrict__ out) {
   __shared__ unsigned long long s_key[GS_SORT_CAP];
   // staged records of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads the
@@ -574,6 +578,7 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
   const bool inside = px < cam.W && py < cam.H;
   bool done = !inside;
   const float pfx = (float)px, pfy = (float)py;
+  const float lim = (OVER && inside) ? depth_lim[(size_t)py * cam.W + px] : 0.0f;
   float T = 1.0f;
   float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
   const char* stage = reinterpret_cast<const char*>(s_stage);
@@ -630,6 +635,10 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
         const float4 a = *reinterpret_cast<const float4*>(stage + o);
         const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
         const float cb = *reinterpret_cast<const float*>(stage + o + 32);
+        if (OVER) {  // sorted by depth: the first Gaussian at or behind the mesh ends the pixel
+          const float gd = *reinterpret_cast<const float*>(stage + o + 44);
+          done = done || !(gd < lim);
+        }
         const float dx = a.x - pfx, dy = a.y - pfy;
         // z = A dx^2 + B dx dy + C dy^2 + log2 o. (The reference's power > 0 skip is not tested: the
         // conic is positive definite (+0.3 low-pass), so power <= 0 up to rounding at power ~ 0.)
@@ -652,14 +661,22 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
       }
     }
   }
-  if (inside) out[(size_t)py * cam.W + px] = make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T);
+  if (inside) {
+    const size_t pix = (size_t)py * cam.W + px;
+    if (OVER) {
+      const float4 u4 = under[pix];
+      out[pix] = make_float4(C0 + T * u4.x, C1 + T * u4.y, C2 + T * u4.z, (1.0f - T) + T * u4.w);
+    } else {
+      out[pix] = make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T);
+    }
+  }
 #endif
 }
 
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
-                           float p11, uint32_t W, uint32_t H, const float bg[3], uint32_t tile_row_begin,
-                           uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, bool time_stages,
-                           hipStream_t s) {
+                           float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
+                           const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
+                           ptgs_splat_stats* stats, bool time_stages, hipStream_t s) {
   hipError_t e;
   if (time_stages && !w->ev[0])
     for (hipEvent_t& ev : w->ev)
@@ -772,11 +789,12 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e2 = mark(4))) return e2;
     if ((e2 = mark(5))) return e2;
     if (rows > 0) {
-      hipLaunchKernelGGL(gs_sort_blend_kernel, dim3(cam.grid_x, rows), dim3(GS_BLOCK), 0, s, cam,
-                         (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
-                         (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p, (const float4*)w->rec.p,
-                         bg[0], bg[1], bg[2], (const uint32_t*)w->total.p, cap, n < (1u << 24) ? 1u : 0u,
-                         (const unsigned long long*)w->tile_slots.p, (float4*)out);
+      auto k = depth ? gs_sort_blend_kernel<true> : gs_sort_blend_kernel<false>;
+      hipLaunchKernelGGL(k, dim3(cam.grid_x, rows), dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p,
+                         (unsigned long long*)w->pairs.p, (unsigned long long*)w->keys_out.p,
+                         (uint32_t*)w->vals_out.p, (const float4*)w->rec.p, bg[0], bg[1], bg[2],
+                         (const uint32_t*)w->total.p, cap, n < (1u << 24) ? 1u : 0u,
+                         (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out);
       if ((e2 = hipGetLastError())) return e2;
     }
     return mark(6);

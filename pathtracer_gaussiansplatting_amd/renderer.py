@@ -100,6 +100,11 @@ class Renderer:
                                        _stream(stream))
         self._chk(rc, "ptgs_trace_torus")
 
+    def trace_depth(self, ubo: Ubo, width: int, height: int, depth, stream=None):
+        """Primary-hit view depth per pixel (+inf on a miss) into a device float[H, W] tensor."""
+        rc = self.lib.ptgs_trace_depth(self._h, C.byref(ubo), width, height, _ptr(depth), _stream(stream))
+        self._chk(rc, "ptgs_trace_depth")
+
     def set_flags(self, flags: int):
         self._chk(self.lib.ptgs_set_flags(self._h, flags), "ptgs_set_flags")
 
@@ -119,7 +124,9 @@ class Renderer:
         self._chk(rc, "ptgs_splat_points")
 
     def splat_gaussians(self, g: dict, ubo: Ubo, width: int, height: int, out, bg=(0.0, 0.0, 0.0),
-                        tile_rows: tuple | None = None, want_stats: bool = False, stream=None):
+                        tile_rows: tuple | None = None, want_stats: bool = False, stream=None, over=None):
+        """over=(depth, under): the hybrid composite of ptgs_splat_gaussians_over (device depth[H, W],
+        under RGBA32F[H, W, 4]; out may be under itself)."""
         gs = Gaussians()
         gs.means, gs.scales, gs.rotations = _ptr(g["means"]), _ptr(g["scales"]), _ptr(g["rotations"])
         gs.opacities, gs.colors = _ptr(g["opacities"]), _ptr(g["colors"])
@@ -127,6 +134,12 @@ class Renderer:
         bgc = np.asarray(bg, np.float32)
         t0, t1 = (0, 0xFFFFFFFF) if tile_rows is None else tile_rows
         st = SplatStats()
+        if over is not None:
+            rc = self.lib.ptgs_splat_gaussians_over(self._h, C.byref(gs), C.byref(ubo), width, height, _ptr(over[0]),
+                                                    _ptr(over[1]), t0, t1, _ptr(out),
+                                                    C.byref(st) if want_stats else None, _stream(stream))
+            self._chk(rc, "ptgs_splat_gaussians_over")
+            return st if want_stats else None
         rc = self.lib.ptgs_splat_gaussians(self._h, C.byref(gs), C.byref(ubo), width, height, _abi.fptr(bgc), t0,
                                            t1, _ptr(out), C.byref(st) if want_stats else None, _stream(stream))
         self._chk(rc, "ptgs_splat_gaussians")
@@ -138,7 +151,7 @@ class Renderer:
         return b
 
     def splat_stage_ms(self) -> np.ndarray:
-        """[preprocess, scan, duplicate, sort, ranges, blend] ms of the last splat (FLAG_TIME_STAGES)."""
+        """[preprocess, count, scatter, 0, 0, sort+blend] ms of the last splat (FLAG_TIME_STAGES)."""
         out = np.zeros(6, np.float32)
         self._chk(self.lib.ptgs_splat_stage_ms(self._h, _abi.fptr(out)), "ptgs_splat_stage_ms")
         return out
