@@ -360,6 +360,21 @@ int ptgs_splat_get_buffers(const ptgs_ctx* ctx, ptgs_splat_buffers* out);
  * [2] scatter (pairs into tile segments) [3] 0 [4] 0 [5] sort + blend. Synchronises. */
 int ptgs_splat_stage_ms(ptgs_ctx* ctx, float out_ms[6]);
 
+/* ---------------- multi-GPU frame reduce over RCCL / xGMI ---------------- */
+/* The path tracer shards samples across GPUs (ptgs_trace_camera with PTGS_ACCUM_SUM and
+ * frame_stride = number of GPUs) and sums the RGBA32F buffers; tile-row shards of the splat are
+ * disjoint and combine with the same sum. One RCCL communicator per context: one rank calls
+ * ptgs_comm_unique_id, the caller ships the 128 bytes to every rank (any channel), each rank calls
+ * ptgs_comm_create with its rank. RCCL is loaded at run time; without it these return PTGS_EHIP. */
+#define PTGS_COMM_ID_BYTES 128
+int ptgs_comm_unique_id(uint8_t id[PTGS_COMM_ID_BYTES]);
+int ptgs_comm_create(ptgs_ctx* ctx, const uint8_t id[PTGS_COMM_ID_BYTES], int nranks, int rank);
+int ptgs_comm_destroy(ptgs_ctx* ctx);
+/* In-place SUM of n_floats device floats: to `root` (ncclReduce) or to every rank (ncclAllReduce).
+ * Stream-ordered on hip_stream. */
+int ptgs_reduce_radiance(ptgs_ctx* ctx, float* accum, size_t n_floats, int root, void* hip_stream);
+int ptgs_allreduce_radiance(ptgs_ctx* ctx, float* accum, size_t n_floats, void* hip_stream);
+
 /* ---------------- output encode (blit rgba32f -> B8G8R8A8_SRGB, engine.cpp:2004-2020) --------- */
 /* rgba8 (device W*H u32, R in the low byte): linear -> sRGB8 of clamp(rgb,0,1), alpha 255. */
 int ptgs_encode_srgb8(ptgs_ctx* ctx, const float* rgba32f, uint32_t width, uint32_t height,

@@ -152,6 +152,11 @@ SYMBOLS = {
     "ptgs_splat_gaussians_over": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _P, _P, _U, _U, _P,
                                        C.POINTER(SplatStats), _P]),
     "ptgs_splat_get_buffers": (_I, [_P, C.POINTER(SplatBuffers)]),
+    "ptgs_comm_unique_id": (_I, [_P]),
+    "ptgs_comm_create": (_I, [_P, _P, C.c_int, C.c_int]),
+    "ptgs_comm_destroy": (_I, [_P]),
+    "ptgs_reduce_radiance": (_I, [_P, _P, C.c_size_t, C.c_int, _P]),
+    "ptgs_allreduce_radiance": (_I, [_P, _P, C.c_size_t, _P]),
     "ptgs_splat_stage_ms": (_I, [_P, _FP]),
     "ptgs_encode_srgb8": (_I, [_P, _P, _U, _U, _P, _P]),
     "ptgs_device_alloc": (_I, [_P, C.c_size_t, C.POINTER(_P)]),

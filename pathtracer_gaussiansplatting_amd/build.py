@@ -20,7 +20,7 @@ INCLUDE = os.path.join(ROOT, "include")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libptgs.so")
 
-SOURCES = ["api.cpp", "bvh.cpp", "scene.cpp", "textures.cpp", "pt_kernels.hip", "raster.hip", "splat.hip"]
+SOURCES = ["api.cpp", "bvh.cpp", "comm.cpp", "scene.cpp", "textures.cpp", "pt_kernels.hip", "raster.hip", "splat.hip"]
 ARCH = os.environ.get("PTGS_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC]
@@ -61,7 +61,7 @@ def build(verbose: bool = False, defines: tuple = (), variant: str = "") -> str:
         return lib
     tmp = lib + ".tmp"
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
-        "-Wl,-Bsymbolic", "-Wl,-rpath,/opt/rocm/lib", "-L/opt/rocm/lib", "-lamdhip64"]
+        "-Wl,-Bsymbolic", "-Wl,-rpath,/opt/rocm/lib", "-L/opt/rocm/lib", "-lamdhip64", "-ldl"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

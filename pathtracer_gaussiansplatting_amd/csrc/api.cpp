@@ -20,6 +20,7 @@
 #include "bvh.h"
 #include "hostmath.h"
 #include "pt_launch.h"
+#include "comm.h"
 #include "splat.h"
 #include "textures.h"
 
@@ -35,6 +36,7 @@ struct ptgs_ctx {
   ptgs_scene_info info{};
   unsigned long long* counters = nullptr;  // 8 x u64
   SplatWorkspace* splat = nullptr;
+  void* comm = nullptr;  // RCCL communicator (ptgs_comm_create)
 };
 
 namespace {
@@ -125,7 +127,57 @@ void ptgs_destroy(ptgs_ctx* c) {
   free_scene(c);
   if (c->counters) (void)hipFree(c->counters);
   splat_workspace_destroy(c->splat);
+  if (c->comm) (void)comm_destroy(c->comm);
   delete c;
+}
+
+int ptgs_comm_unique_id(uint8_t id[PTGS_COMM_ID_BYTES]) {
+  if (!id) return PTGS_EINVAL;
+  if (!comm_available()) return PTGS_EHIP;
+  return comm_unique_id(id) == 0 ? PTGS_OK : PTGS_EHIP;
+}
+
+int ptgs_comm_create(ptgs_ctx* c, const uint8_t id[PTGS_COMM_ID_BYTES], int nranks, int rank) {
+  if (!c || !id) return PTGS_EINVAL;
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(c, PTGS_EINVAL, "bad rank %d of %d", rank, nranks);
+  if (!comm_available()) return fail(c, PTGS_EHIP, "RCCL (librccl.so.1) could not be loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->comm) {
+    (void)comm_destroy(c->comm);
+    c->comm = nullptr;
+  }
+  int e = comm_create(id, nranks, rank, &c->comm);
+  if (e) return fail(c, PTGS_EHIP, "ncclCommInitRank: %s", comm_error(e));
+  return PTGS_OK;
+}
+
+int ptgs_comm_destroy(ptgs_ctx* c) {
+  if (!c) return PTGS_EINVAL;
+  if (c->comm) {
+    int e = comm_destroy(c->comm);
+    c->comm = nullptr;
+    if (e) return fail(c, PTGS_EHIP, "ncclCommDestroy: %s", comm_error(e));
+  }
+  return PTGS_OK;
+}
+
+static int reduce_common(ptgs_ctx* c, float* accum, size_t n, int root, bool all, void* stream) {
+  if (!c || !accum) return PTGS_EINVAL;
+  if (!c->comm) return fail(c, PTGS_EINVAL, "no communicator (ptgs_comm_create)");
+  if (!is_device_ptr(accum)) return fail(c, PTGS_EINVAL, "accum is not a device pointer");
+  HIPCHK(c, hipSetDevice(c->device));
+  int e = all ? comm_allreduce_sum(c->comm, accum, n, (hipStream_t)stream)
+              : comm_reduce_sum(c->comm, accum, n, root, (hipStream_t)stream);
+  if (e) return fail(c, PTGS_EHIP, "%s: %s", all ? "ncclAllReduce" : "ncclReduce", comm_error(e));
+  return PTGS_OK;
+}
+
+int ptgs_reduce_radiance(ptgs_ctx* c, float* accum, size_t n_floats, int root, void* stream) {
+  return reduce_common(c, accum, n_floats, root, false, stream);
+}
+
+int ptgs_allreduce_radiance(ptgs_ctx* c, float* accum, size_t n_floats, void* stream) {
+  return reduce_common(c, accum, n_floats, 0, true, stream);
 }
 
 const char* ptgs_last_error(const ptgs_ctx* c) { return c ? c->err.c_str() : "null context"; }

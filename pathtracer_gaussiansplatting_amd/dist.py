@@ -49,6 +49,20 @@ def all_reduce_sum(tensor, group=None):
     return tensor
 
 
+def init_native_comm(renderer, group=None):
+    """The library's own RCCL communicator (ptgs_comm_create) on every rank: rank 0 makes the unique
+    id, torch.distributed ships it (any backend). After this, renderer.reduce_radiance /
+    allreduce_radiance run the frame reduce through the C-ABI instead of torch."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    box = [renderer.comm_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(box, src=0, group=group)
+    renderer.comm_create(box[0], world, rank)
+    return rank, world
+
+
 def resolve_mean(sum_rgba):
     """rgb / count, alpha = 1 (the running-mean image the reference keeps in rt_output_image)."""
     out = sum_rgba.clone()

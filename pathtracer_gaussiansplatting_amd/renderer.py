@@ -105,6 +105,27 @@ class Renderer:
         rc = self.lib.ptgs_trace_depth(self._h, C.byref(ubo), width, height, _ptr(depth), _stream(stream))
         self._chk(rc, "ptgs_trace_depth")
 
+    # ---------------------------------------------------------------- RCCL frame reduce (§8e)
+    def comm_unique_id(self) -> bytes:
+        buf = (C.c_uint8 * 128)()
+        self._chk(self.lib.ptgs_comm_unique_id(buf), "ptgs_comm_unique_id")
+        return bytes(buf)
+
+    def comm_create(self, unique_id: bytes, nranks: int, rank: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._chk(self.lib.ptgs_comm_create(self._h, buf, nranks, rank), "ptgs_comm_create")
+
+    def comm_destroy(self):
+        self._chk(self.lib.ptgs_comm_destroy(self._h), "ptgs_comm_destroy")
+
+    def reduce_radiance(self, accum, root: int = 0, stream=None):
+        rc = self.lib.ptgs_reduce_radiance(self._h, _ptr(accum), accum.numel(), root, _stream(stream))
+        self._chk(rc, "ptgs_reduce_radiance")
+
+    def allreduce_radiance(self, accum, stream=None):
+        rc = self.lib.ptgs_allreduce_radiance(self._h, _ptr(accum), accum.numel(), _stream(stream))
+        self._chk(rc, "ptgs_allreduce_radiance")
+
     def set_flags(self, flags: int):
         self._chk(self.lib.ptgs_set_flags(self._h, flags), "ptgs_set_flags")
 

@@ -89,3 +89,11 @@ def test_missing_library_fails_loudly(tmp_path):
     from pathtracer_gaussiansplatting_amd import _abi
     with pytest.raises(_abi.PtgsError):
         _abi.load_library(str(tmp_path / "libptgs.so"))
+
+
+def test_rccl_unique_id_without_gpu(native_lib):
+    """The RCCL bootstrap id needs no device: the C-ABI resolves librccl at run time."""
+    buf = (C.c_uint8 * 128)()
+    assert native_lib.ptgs_comm_unique_id(buf) == 0
+    assert any(bytes(buf))
+    assert native_lib.ptgs_comm_unique_id(None) == -1  # PTGS_EINVAL

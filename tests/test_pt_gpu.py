@@ -123,3 +123,18 @@ def test_row_range(renderer, oracle_lib):
     o, so = _oracle_render(oracle_lib, sc, ubo, 64, 64, 1, rows=(10, 37))
     _compare(g, o, sg, so)
     assert np.all(g[:10] == 0) and np.all(g[37:] == 0)
+
+
+def test_native_rccl_reduce_single_rank(renderer):
+    """ptgs_comm_create / ptgs_reduce_radiance / ptgs_allreduce_radiance through the C-ABI on a
+    one-rank RCCL communicator (the box has one GPU): the SUM over one rank is the identity."""
+    from pathtracer_gaussiansplatting_amd import dist as D
+    rank, world = D.init_native_comm(renderer)
+    assert (rank, world) == (0, 1)
+    x = torch.arange(4096 * 4, dtype=torch.float32, device="cuda").reshape(4096, 4)
+    ref = x.clone()
+    renderer.reduce_radiance(x, root=0)
+    renderer.allreduce_radiance(x)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+    renderer.comm_destroy()
