@@ -360,6 +360,30 @@ int ptgs_splat_get_buffers(const ptgs_ctx* ctx, ptgs_splat_buffers* out);
  * [2] scatter (pairs into tile segments) [3] 0 [4] 0 [5] sort + blend. Synchronises. */
 int ptgs_splat_stage_ms(ptgs_ctx* ctx, float out_ms[6]);
 
+/* ---------------- dataset capture (Engine::captureSceneData, engine.cpp:2658-2814) -------- */
+typedef struct ptgs_capture_desc {
+    const char* out_dir;            /* writes out_dir/train/r_<i>.jpg, transforms_{train,test}.json, points3d.ply */
+    uint32_t width, height;         /* render size (the reference's swapchain extent) */
+    uint32_t total_positions;       /* camera views (settings "total_positions", default 336) */
+    uint32_t accumulation_steps;    /* samples per view and torus frames (settings default 512) */
+    float min_beta, max_beta;       /* torus elevation range, degrees (defaults -45, 45) */
+    float fov_deg;                  /* camera fov (60) */
+    float major_radius, torus_height; /* Camera::updateToroidalAngles radius / height */
+    float image_divisor;            /* > 1: every 2nd pixel is kept (engine.cpp:2737-2754) */
+    uint32_t seed;                  /* mt19937 seed (13) */
+    uint32_t capture_images, capture_pointcloud;
+    const ptgs_ubo* ubo;            /* template: ambient light, fluxes, lod settings (view/proj/frame set per view) */
+    ptgs_ray_push torus;            /* torus push constants for the point cloud */
+    const ptgs_ray_sample* samples; /* device array (Morton-sorted RaySamples), num_samples entries */
+    uint32_t num_samples;
+    void* hip_stream;
+} ptgs_capture_desc;
+
+/* Synchronous: traces every view (one batched ptgs_trace_camera call of accumulation_steps samples per
+ * view), encodes/reads back/downsamples/writes JPEG quality 90, accumulates the torus point cloud,
+ * writes the PLY and the two transforms files. Requires an uploaded scene. */
+int ptgs_capture_dataset(ptgs_ctx* ctx, const ptgs_capture_desc* desc);
+
 /* ---------------- multi-GPU frame reduce over RCCL / xGMI ---------------- */
 /* The path tracer shards samples across GPUs (ptgs_trace_camera with PTGS_ACCUM_SUM and
  * frame_stride = number of GPUs) and sums the RGBA32F buffers; tile-row shards of the splat are

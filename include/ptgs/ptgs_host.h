@@ -30,6 +30,23 @@ int ptgs_camera_lookat(const float eye[3], const float center[3], const float up
 int ptgs_camera_perspective(float fovy_rad, float aspect, float near_plane, float far_plane, float proj[16]);
 /* column-major 4x4 inverse (double internally, rounded once) */
 int ptgs_mat4_inverse(const float m[16], float out[16]);
+/* glm::inverse(mat4) in float, GLM 0.9.9 compute_inverse restated operation for operation (what the
+ * reference writes into transforms.json, engine.cpp:2760) */
+int ptgs_mat4_inverse_glm(const float m[16], float out[16]);
+
+/* ----- capture writers (engine.cpp:2672-2681, :2816-2895; GeneralHeaders.cpp:178-190) ----- */
+/* n (alpha, beta) pairs in degrees from std::mt19937(seed) + uniform_real_distribution<double>:
+ * alpha U(0, 360) then beta U(min_beta, max_beta), each rounded to float */
+int ptgs_capture_poses(uint32_t n, uint32_t seed, float min_beta, float max_beta, float* alpha_beta);
+/* nlohmann::json dump(4) layout: camera_angle_x = 2 atan(tan(fov_y / 2) aspect), frames with file_path
+ * and transform_matrix rows (transforms: n column-major 4x4) */
+int ptgs_write_transforms_json(const char* path, float fov_y_deg, float aspect, uint32_t n,
+                               const char* const* file_paths, const float* transforms);
+/* ASCII PLY of the points with flag > 0 (Engine::savePly); num_written may be NULL */
+int ptgs_write_ply(const char* path, const ptgs_hitdata* hits, uint32_t n, uint32_t* num_written);
+/* baseline JFIF; comp 1/3/4 (alpha ignored); quality 1..100 (the reference uses 90) */
+int ptgs_write_jpeg(const char* path, const uint8_t* pixels, uint32_t width, uint32_t height, uint32_t comp,
+                    int quality);
 
 /* ----- scene builder ----- */
 typedef struct ptgs_scene_builder ptgs_scene_builder;

@@ -81,6 +81,15 @@ class RayPush(C.Structure):
                 ("minor_radius", C.c_float), ("height", C.c_float)]
 
 
+class CaptureDesc(C.Structure):
+    _fields_ = [("out_dir", C.c_char_p), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("total_positions", C.c_uint32), ("accumulation_steps", C.c_uint32), ("min_beta", C.c_float),
+                ("max_beta", C.c_float), ("fov_deg", C.c_float), ("major_radius", C.c_float),
+                ("torus_height", C.c_float), ("image_divisor", C.c_float), ("seed", C.c_uint32),
+                ("capture_images", C.c_uint32), ("capture_pointcloud", C.c_uint32), ("ubo", C.c_void_p),
+                ("torus", RayPush), ("samples", C.c_void_p), ("num_samples", C.c_uint32), ("hip_stream", C.c_void_p)]
+
+
 class SceneDesc(C.Structure):
     _fields_ = [("vertices", C.c_void_p), ("num_vertices", C.c_uint32), ("indices", C.c_void_p),
                 ("num_indices", C.c_uint32), ("meshes", C.c_void_p), ("mesh_index_count", C.c_void_p),
@@ -170,6 +179,12 @@ SYMBOLS = {
     "ptgs_camera_lookat": (_I, [_FP, _FP, _FP, _FP]),
     "ptgs_camera_perspective": (_I, [C.c_float] * 4 + [_FP]),
     "ptgs_mat4_inverse": (_I, [_FP, _FP]),
+    "ptgs_mat4_inverse_glm": (_I, [_FP, _FP]),
+    "ptgs_capture_poses": (_I, [_U, _U, C.c_float, C.c_float, _FP]),
+    "ptgs_write_transforms_json": (_I, [C.c_char_p, C.c_float, C.c_float, _U, C.POINTER(C.c_char_p), _FP]),
+    "ptgs_write_ply": (_I, [C.c_char_p, _P, _U, C.POINTER(C.c_uint32)]),
+    "ptgs_write_jpeg": (_I, [C.c_char_p, _P, _U, _U, _U, C.c_int]),
+    "ptgs_capture_dataset": (_I, [_P, _P]),
     "ptgs_builder_create": (_I, [C.POINTER(_P)]),
     "ptgs_builder_destroy": (None, [_P]),
     "ptgs_builder_add_rtbox_json": (_I, [_P, C.c_char_p]),
