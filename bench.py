@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--no-gs", action="store_true")
     ap.add_argument("--no-pt", action="store_true")
     ap.add_argument("--no-hybrid", action="store_true")
+    ap.add_argument("--no-gpu-bvh", action="store_true")
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
     ap.add_argument("--hybrid-spp", type=int, default=16)
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented counting pass")
@@ -86,7 +87,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
-    from pathtracer_gaussiansplatting_amd import (ACCUM_RUNNING_MEAN, ACCUM_SUM, FLAG_COUNT_TRAVERSAL,
+    from pathtracer_gaussiansplatting_amd import (ACCUM_RUNNING_MEAN, ACCUM_SUM, FLAG_COUNT_TRAVERSAL, FLAG_GPU_BVH,
                                                   FLAG_TIME_STAGES, Camera, Renderer, make_ubo)
     from pathtracer_gaussiansplatting_amd import synthetic as Y
 
@@ -180,6 +181,7 @@ def main():
             "config": {"workload": f"C3 path trace: {args.triangles}-tri Sponza-like atrium, {W}x{H}, {SPP} spp per GPU",
                        "width": W, "height": H, "spp_per_gpu": SPP, "triangles": int(info.num_triangles),
                        "bvh_nodes": int(info.num_bvh_nodes), "bvh_depth": int(info.bvh_depth),
+                       "bvh_build": f"host binned SAH, {info.build_ms:.1f} ms",
                        "parallelism": "single GPU" if world == 1 else f"sample-shard x{world} + RCCL reduce"},
             "rays_per_step": rays_total / args.steps,
             "samples_per_s": st.samples * world / dt_max,
@@ -196,6 +198,26 @@ def main():
             "roofline_l2": {"bound": "l2", "achieved": round(achieved, 2), "peak": L2_PEAK_GBS, "unit": "GB/s",
                             "frac": round(achieved / L2_PEAK_GBS, 5)},
         })
+        # the GPU LBVH builder (PTGS_FLAG_GPU_BVH) on the same scene: build time and one traced frame
+        if world == 1 and not args.no_gpu_bvh:
+            r.set_flags(FLAG_GPU_BVH)
+            r.upload_scene(scene)  # first build pays hipCUB / module first-use costs
+            ginfo = r.upload_scene(scene)
+            r.set_flags(0)
+            pt_step()
+            torch.cuda.synchronize()
+            r.stats_reset(stream)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pt_step()
+            torch.cuda.synchronize()
+            gdt_pt = time.perf_counter() - t0
+            gst = r.stats()
+            out["bvh_gpu"] = {"build_ms": round(float(ginfo.build_ms), 3), "nodes": int(ginfo.num_bvh_nodes),
+                              "depth": int(ginfo.bvh_depth),
+                              "mrays_per_s": round((gst.extension_rays + gst.shadow_rays) / gdt_pt / 1e6, 2),
+                              "note": "LBVH built on the GPU (fast rebuilds); the headline value uses the host SAH BVH"}
+            r.upload_scene(scene)  # back to the SAH tree for the legs below
         del accum
 
     # ------------------------------------------------------------------ 3DGS (C2)

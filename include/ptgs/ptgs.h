@@ -283,6 +283,9 @@ typedef struct ptgs_trace_stats {
 
 #define PTGS_FLAG_COUNT_TRAVERSAL 1u /* instrumented kernels: node / triangle / hit counters */
 #define PTGS_FLAG_TIME_STAGES 2u     /* hipEvent timing of the splat pipeline stages */
+#define PTGS_FLAG_GPU_BVH 4u         /* ptgs_scene_upload builds the BVH on the GPU (LBVH; fast rebuilds,
+                                      * slower traversal than the default host SAH build); falls back to
+                                      * the host build when the tree exceeds the traversal stack depth */
 int ptgs_set_flags(ptgs_ctx* ctx, uint32_t flags);
 int ptgs_stats_reset(ptgs_ctx* ctx, void* hip_stream);
 int ptgs_stats_read(ptgs_ctx* ctx, ptgs_trace_stats* out); /* synchronises the context's device */

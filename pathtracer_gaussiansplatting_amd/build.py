@@ -20,7 +20,7 @@ INCLUDE = os.path.join(ROOT, "include")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libptgs.so")
 
-SOURCES = ["api.cpp", "bvh.cpp", "capture.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp", "pt_kernels.hip", "raster.hip", "splat.hip"]
+SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "capture.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp", "pt_kernels.hip", "raster.hip", "splat.hip"]
 ARCH = os.environ.get("PTGS_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC]

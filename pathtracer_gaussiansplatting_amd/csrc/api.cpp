@@ -18,6 +18,7 @@
 
 #include "../../include/ptgs/ptgs.h"
 #include "bvh.h"
+#include "bvh_gpu.h"
 #include "hostmath.h"
 #include "pt_launch.h"
 #include "comm.h"
@@ -242,19 +243,50 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     }
   }
 
-  auto t0 = std::chrono::steady_clock::now();
-  BvhOut bvh;
-  build_bvh(tris, 4, PTGS_STACK - 1, bvh);
-  auto t1 = std::chrono::steady_clock::now();
-  if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
-
   free_scene(c);
   c->info = ptgs_scene_info{};
   DevScene s{};
   int rc;
-  if ((rc = upload(c, (const float4*)bvh.nodes.data(), bvh.nodes.size() / 4, &s.nodes))) return rc;
-  if ((rc = upload(c, (const float4*)bvh.tris.data(), bvh.tris.size() / 4, &s.tris))) return rc;
-  if ((rc = upload(c, bvh.tri_flags.data(), bvh.tri_flags.size(), &s.tri_flags))) return rc;
+  // BVH: the host binned-SAH build (default), or with PTGS_FLAG_GPU_BVH the GPU LBVH (bvh_gpu.hip),
+  // falling back to the host build when the LBVH is deeper than the traversal stack
+  bool built = false;
+  if ((c->flags & PTGS_FLAG_GPU_BVH) && tris.size() >= 16) {
+    GpuBvh g;
+    float ms = 0.0f;
+    hipError_t e = build_bvh_gpu(tris, PTGS_STACK - 1, g, &ms);
+    if (e == hipSuccess) {
+      for (void* p : {(void*)g.nodes, (void*)g.tris, (void*)g.tri_flags}) c->scene_allocs.push_back(p);
+      s.nodes = g.nodes;
+      s.tris = g.tris;
+      s.tri_flags = g.tri_flags;
+      c->info.num_bvh_nodes = g.num_nodes;
+      c->info.bvh_depth = g.depth;
+      c->info.max_leaf_size = 4;
+      c->info.build_ms = ms;
+      c->info.device_bytes += (size_t)g.num_nodes * 64 + tris.size() * 52;
+      built = true;
+    } else if (e == hipErrorNotSupported) {
+      (void)hipFree(g.nodes);
+      (void)hipFree(g.tris);
+      (void)hipFree(g.tri_flags);
+    } else {
+      return fail(c, PTGS_EHIP, "GPU BVH build: %s", hipGetErrorString(e));
+    }
+  }
+  if (!built) {
+    auto t0 = std::chrono::steady_clock::now();
+    BvhOut bvh;
+    build_bvh(tris, 4, PTGS_STACK - 1, bvh);
+    auto t1 = std::chrono::steady_clock::now();
+    if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
+    if ((rc = upload(c, (const float4*)bvh.nodes.data(), bvh.nodes.size() / 4, &s.nodes))) return rc;
+    if ((rc = upload(c, (const float4*)bvh.tris.data(), bvh.tris.size() / 4, &s.tris))) return rc;
+    if ((rc = upload(c, bvh.tri_flags.data(), bvh.tri_flags.size(), &s.tri_flags))) return rc;
+    c->info.num_bvh_nodes = bvh.num_nodes;
+    c->info.bvh_depth = bvh.depth;
+    c->info.max_leaf_size = bvh.max_leaf;
+    c->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  }
   // a zero vertex/index count still needs valid (never dereferenced) pointers
   ptgs_vertex dummy_v{};
   uint32_t dummy_i = 0;
@@ -287,10 +319,6 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
   c->dsc = s;
   c->has_scene = true;
   c->info.num_triangles = (uint32_t)tris.size();
-  c->info.num_bvh_nodes = bvh.num_nodes;
-  c->info.bvh_depth = bvh.depth;
-  c->info.max_leaf_size = bvh.max_leaf;
-  c->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   return PTGS_OK;
 }
 

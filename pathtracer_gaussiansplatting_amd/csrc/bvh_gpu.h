@@ -1,0 +1,24 @@
+// bvh_gpu.h — GPU LBVH builder (bvh_gpu.hip) producing the device layout of bvh.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "bvh.h"
+
+namespace ptgs {
+
+struct GpuBvh {
+  float4* nodes = nullptr;       // 4 float4 per interior node
+  float4* tris = nullptr;        // 3 float4 per triangle, leaf order
+  uint32_t* tri_flags = nullptr;
+  uint32_t num_nodes = 0;
+  uint32_t depth = 0;
+};
+
+// n >= 2 triangles. hipErrorNotSupported: the tree is deeper than max_depth (out holds it; free it
+// and build on the host). build_ms: device time of the build kernels.
+hipError_t build_bvh_gpu(const std::vector<BuildTri>& tris, uint32_t max_depth, GpuBvh& out, float* build_ms);
+
+}  // namespace ptgs

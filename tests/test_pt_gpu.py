@@ -138,3 +138,26 @@ def test_native_rccl_reduce_single_rank(renderer):
     torch.cuda.synchronize()
     assert torch.equal(x, ref)
     renderer.comm_destroy()
+
+
+@pytest.mark.parametrize("scene", ["features", "atrium"])
+def test_gpu_bvh_builder_same_image(renderer, scene):
+    """PTGS_FLAG_GPU_BVH (LBVH built on the GPU) renders the image of the host SAH BVH bit for bit:
+    hits do not depend on the tree (closest-hit tie rule, conservative boxes)."""
+    from pathtracer_gaussiansplatting_amd import FLAG_GPU_BVH
+    sc = U.features() if scene == "features" else U.atrium()
+    pose = U.cornell_pose(160 / 120) if scene == "features" else U.atrium_pose()
+    ubo = make_ubo(pose, sc, 0, ambient=(0.3, 0.4, 0.5, 1.0))
+    host, st_h = _gpu_render(renderer, sc, ubo, 160, 120, 2)
+    info_h = renderer.scene_info()
+    renderer.set_flags(FLAG_GPU_BVH)
+    try:
+        gpu, st_g = _gpu_render(renderer, sc, ubo, 160, 120, 2)
+        info_g = renderer.scene_info()
+    finally:
+        renderer.set_flags(0)
+    assert np.array_equal(gpu, host)
+    assert st_g.extension_rays == st_h.extension_rays and st_g.shadow_rays == st_h.shadow_rays
+    assert info_g.num_triangles == info_h.num_triangles and info_g.bvh_depth <= 31
+    print(f"{scene}: host SAH {info_h.build_ms:.1f} ms ({info_h.num_bvh_nodes} nodes, depth {info_h.bvh_depth}), "
+          f"GPU LBVH {info_g.build_ms:.2f} ms ({info_g.num_bvh_nodes} nodes, depth {info_g.bvh_depth})")
