@@ -8,6 +8,7 @@
  *   objects : Gameobject emissive-triangle extraction           Vulkan_Engine/gameobject.cpp:567, :777-790
  *   flatten : Engine::createGlobalBindlessBuffers               Vulkan_Engine/engine.cpp:1658-1860
  *   export  : Engine::saveTransformsJson / savePly              Vulkan_Engine/engine.cpp:2816-2895
+ *   ingest  : Gameobject::loadModel (glTF) / Engine::loadScene   gameobject.cpp:198-851, engine.cpp:1172-1352
  * Pure host code (no GPU needed).
  */
 #ifndef PTGS_HOST_H_
@@ -75,6 +76,64 @@ int ptgs_builder_add_object(ptgs_scene_builder* b, const ptgs_vertex* vertices, 
  * total_flux, p_emissive). */
 int ptgs_builder_finalize(ptgs_scene_builder* b, ptgs_scene_desc* desc, ptgs_ubo* ubo);
 const char* ptgs_builder_last_error(const ptgs_scene_builder* b);
+
+/* ----- scene ingest (§8f #3) ----- */
+/* Decode a PNG / JPEG image held in memory to RGBA8 with the semantics of
+ * stbi_load(..., STBI_rgb_alpha) (Image::createTextureImage, Vulkan_Engine/image.cpp:12).
+ * rgba = NULL queries width / height / comp (channels in the file) only; PTGS_ERANGE when
+ * capacity < width * height * 4; PTGS_EIO on malformed or unsupported data. */
+int ptgs_image_decode_rgba8(const void* bytes, size_t size, uint8_t* rgba, size_t capacity, uint32_t* width,
+                            uint32_t* height, uint32_t* comp);
+
+/* substitute a 1x1 white texture for an image file that is missing or undecodable (the reference
+ * throws "failed to load texture image", image.cpp:19-21) */
+#define PTGS_INGEST_MISSING_IMAGES_WHITE 1u
+
+/* One glTF 2.0 model (.gltf with external or data: buffers, or .glb) as one Gameobject
+ * (Gameobject::loadModel, gameobject.cpp:198-851): frame-0 node transforms and CPU skinning,
+ * KHR_lights_punctual, materials incl. KHR_materials_{pbrSpecularGlossiness, emissive_strength,
+ * specular, transmission, clearcoat} and KHR_texture_transform, every image decoded (sRGB unless
+ * only used as a linear map), vertex dedup and the duplicated index copy of the reference.
+ * Then the scene-JSON placement is baked in (engine.cpp:1271-1331): translate(position) *
+ * quat(radians(rotation_deg)) * scale(scale); NULL = 0 / 0 / 1. Returns PTGS_EIO with
+ * ptgs_builder_last_error() set on any load failure. */
+int ptgs_builder_add_gltf(ptgs_scene_builder* b, const char* path, const float position[3],
+                          const float rotation_deg[3], const float scale[3], uint32_t flags);
+/* A scene-level light placed before every object light and never filtered (the settings "sun",
+ * engine.cpp:1225-1242). */
+int ptgs_builder_add_punctual_light(ptgs_scene_builder* b, const ptgs_punctual_light* light);
+
+/* Engine::loadScene settings (engine.cpp:1190-1255) with the Engine defaults for absent keys */
+typedef struct ptgs_scene_settings {
+    float ambient_light[4];      /* default (0, 0, 0, 1) */
+    int32_t use_rt_box;
+    int32_t render_torus;        /* default 1 */
+    int32_t render_pointcloud;   /* default 1 */
+    float torus_major_radius;    /* 16 */
+    float torus_minor_radius;    /* 1 */
+    float torus_height;          /* 8 */
+    int32_t torus_major_segments;
+    int32_t torus_minor_segments;
+    uint32_t num_rays;           /* 1000000 */
+    float use_lod;               /* 0 */
+    float lod_factor;            /* 1 */
+    uint32_t accumulation_steps; /* 512 */
+    uint32_t total_positions;    /* 336 */
+    float min_beta;              /* -45 */
+    float max_beta;              /* 45 */
+    float image_divisor;         /* 2 */
+    int32_t capture_images;      /* 1 */
+    int32_t capture_pointcloud;  /* 1 */
+    uint32_t num_objects;        /* models loaded */
+} ptgs_scene_settings;
+
+/* Engine::loadScene (engine.cpp:1172-1352): `path` is either the scene JSON itself or a file whose
+ * "scene" key names it (main_scene.json). Model / rt-box paths in the JSON are resolved against
+ * root_dir (the reference resolves them against its working directory; NULL = as given). Objects are
+ * appended in order, then the rt-box when settings.use_rt_box; the "sun" replaces the builder's
+ * scene-level lights. settings may be NULL. */
+int ptgs_builder_load_scene_json(ptgs_scene_builder* b, const char* path, const char* root_dir, uint32_t flags,
+                                 ptgs_scene_settings* settings);
 
 #ifdef __cplusplus
 }

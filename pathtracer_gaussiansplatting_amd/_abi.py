@@ -106,6 +106,21 @@ class Texture(C.Structure):
                 ("reserved", C.c_uint32)]
 
 
+class SceneSettings(C.Structure):
+    """ptgs_scene_settings: Engine::loadScene settings (engine.cpp:1190-1255)."""
+    _fields_ = [("ambient_light", C.c_float * 4), ("use_rt_box", C.c_int32), ("render_torus", C.c_int32),
+                ("render_pointcloud", C.c_int32), ("torus_major_radius", C.c_float),
+                ("torus_minor_radius", C.c_float), ("torus_height", C.c_float),
+                ("torus_major_segments", C.c_int32), ("torus_minor_segments", C.c_int32),
+                ("num_rays", C.c_uint32), ("use_lod", C.c_float), ("lod_factor", C.c_float),
+                ("accumulation_steps", C.c_uint32), ("total_positions", C.c_uint32), ("min_beta", C.c_float),
+                ("max_beta", C.c_float), ("image_divisor", C.c_float), ("capture_images", C.c_int32),
+                ("capture_pointcloud", C.c_int32), ("num_objects", C.c_uint32)]
+
+
+INGEST_MISSING_IMAGES_WHITE = 1
+
+
 class SceneInfo(C.Structure):
     _fields_ = [("num_triangles", C.c_uint32), ("num_bvh_nodes", C.c_uint32), ("bvh_depth", C.c_uint32),
                 ("max_leaf_size", C.c_uint32), ("build_ms", C.c_double), ("device_bytes", C.c_uint64)]
@@ -192,6 +207,10 @@ SYMBOLS = {
     "ptgs_builder_add_object": (_I, [_P, _P, _U, _P, _U, _P, _U, _P, _U, _P, _U, _U]),
     "ptgs_builder_finalize": (_I, [_P, C.POINTER(SceneDesc), C.POINTER(Ubo)]),
     "ptgs_builder_last_error": (C.c_char_p, [_P]),
+    "ptgs_image_decode_rgba8": (_I, [_P, C.c_size_t, _P, C.c_size_t, C.POINTER(_U), C.POINTER(_U), C.POINTER(_U)]),
+    "ptgs_builder_add_gltf": (_I, [_P, C.c_char_p, _FP, _FP, _FP, _U]),
+    "ptgs_builder_add_punctual_light": (_I, [_P, _P]),
+    "ptgs_builder_load_scene_json": (_I, [_P, C.c_char_p, C.c_char_p, _U, C.POINTER(SceneSettings)]),
 }
 
 _lib = None

@@ -20,7 +20,10 @@ INCLUDE = os.path.join(ROOT, "include")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libptgs.so")
 
-SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "capture.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp", "pt_kernels.hip", "raster.hip", "splat.hip"]
+SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "capture.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp",
+           "pt_kernels.hip", "raster.hip", "splat.hip", "gltf.cpp", "image_decode.cpp"]
+# pure host code (scene ingest): plain g++, no device pass
+HOST_SOURCES = {"gltf.cpp", "image_decode.cpp"}
 ARCH = os.environ.get("PTGS_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC]
@@ -42,7 +45,9 @@ def _compile(src: str, defines: tuple = (), build_dir: str = BUILD) -> str:
         return obj
     dflags = [f"-D{d}" for d in defines]
     cmd = [_hipcc()] + COMMON + dflags + [f"--offload-arch={ARCH}", "-c", path, "-o", obj]
-    if src.endswith(".cpp"):
+    if src in HOST_SOURCES:
+        cmd = ["g++"] + COMMON + dflags + ["-c", path, "-o", obj]
+    elif src.endswith(".cpp"):
         cmd = [_hipcc()] + COMMON + dflags + ["-x", "hip", f"--offload-arch={ARCH}", "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -61,7 +66,7 @@ def build(verbose: bool = False, defines: tuple = (), variant: str = "") -> str:
         return lib
     tmp = lib + ".tmp"
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
-        "-Wl,-Bsymbolic", "-Wl,-rpath,/opt/rocm/lib", "-L/opt/rocm/lib", "-lamdhip64", "-ldl"]
+        "-Wl,-Bsymbolic", "-Wl,-rpath,/opt/rocm/lib", "-L/opt/rocm/lib", "-lamdhip64", "-ldl", "-lz"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -12,6 +12,11 @@
 
 #include "../../include/ptgs/ptgs_host.h"
 #include "hostmath.h"
+#include "json.h"
+#include "scene_builder.h"
+
+using ptgs::JVal;
+using ptgs::jnum;
 
 namespace {
 
@@ -73,116 +78,10 @@ f3 rotate_dir(float angle, f3 axis_in, f3 v) {
           (R[0][2] * v.x + R[1][2] * v.y) + R[2][2] * v.z};
 }
 
-// ---------------------------------------------------------------------------------------------
-// minimal JSON reader (objects, arrays, numbers, strings, bools, null)
-// ---------------------------------------------------------------------------------------------
-struct JVal {
-  enum Kind { NUL, BOOL, NUM, STR, ARR, OBJ } kind = NUL;
-  double num = 0;
-  bool b = false;
-  std::string str;
-  std::vector<JVal> arr;
-  std::map<std::string, JVal> obj;
-  const JVal* get(const std::string& k) const {
-    if (kind != OBJ) return nullptr;
-    auto it = obj.find(k);
-    return it == obj.end() ? nullptr : &it->second;
-  }
-};
-
-struct JParser {
-  const char* p;
-  const char* end;
-  bool ok = true;
-  void ws() { while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p; }
-  bool lit(const char* s) {
-    size_t n = strlen(s);
-    if ((size_t)(end - p) >= n && strncmp(p, s, n) == 0) { p += n; return true; }
-    return false;
-  }
-  JVal parse() {
-    JVal v;
-    ws();
-    if (p >= end) { ok = false; return v; }
-    if (*p == '{') {
-      ++p; v.kind = JVal::OBJ; ws();
-      if (p < end && *p == '}') { ++p; return v; }
-      while (ok) {
-        ws();
-        JVal k = parse();
-        if (k.kind != JVal::STR) { ok = false; break; }
-        ws();
-        if (p >= end || *p != ':') { ok = false; break; }
-        ++p;
-        v.obj[k.str] = parse();
-        ws();
-        if (p < end && *p == ',') { ++p; continue; }
-        if (p < end && *p == '}') { ++p; break; }
-        ok = false;
-      }
-    } else if (*p == '[') {
-      ++p; v.kind = JVal::ARR; ws();
-      if (p < end && *p == ']') { ++p; return v; }
-      while (ok) {
-        v.arr.push_back(parse());
-        ws();
-        if (p < end && *p == ',') { ++p; continue; }
-        if (p < end && *p == ']') { ++p; break; }
-        ok = false;
-      }
-    } else if (*p == '"') {
-      ++p; v.kind = JVal::STR;
-      while (p < end && *p != '"') {
-        if (*p == '\\' && p + 1 < end) { ++p; v.str.push_back(*p == 'n' ? '\n' : *p); ++p; }
-        else v.str.push_back(*p++);
-      }
-      if (p < end) ++p; else ok = false;
-    } else if (lit("true")) { v.kind = JVal::BOOL; v.b = true; }
-    else if (lit("false")) { v.kind = JVal::BOOL; v.b = false; }
-    else if (lit("null")) { v.kind = JVal::NUL; }
-    else {
-      char* e = nullptr;
-      v.num = strtod(p, &e);
-      if (e == p) { ok = false; return v; }
-      v.kind = JVal::NUM;
-      p = e;
-    }
-    return v;
-  }
-};
-
-float jnum(const JVal* v, float def) { return (v && v->kind == JVal::NUM) ? (float)v->num : def; }
-
 }  // namespace
 
-struct ptgs_scene_builder {
-  struct Object {
-    std::vector<ptgs_vertex> vertices;
-    std::vector<uint32_t> indices;
-    std::vector<ptgs_primitive> prims;
-    std::vector<ptgs_material> materials;  // texture ids object-relative, pad = is_transparent
-    std::vector<ptgs_punctual_light> lights;
-    struct ETri { uint32_t i0, i1, i2, mat; float area; };
-    std::vector<ETri> etris;
-    uint32_t num_textures = 1;
-  };
-  std::vector<Object> objects;
-  bool has_rtbox = false;
-  Object rtbox;
-  std::string err;
-  // finalized arrays
-  std::vector<ptgs_vertex> v;
-  std::vector<uint32_t> idx;
-  std::vector<ptgs_mesh_info> meshes;
-  std::vector<uint32_t> mesh_count;
-  std::vector<ptgs_material> mats;
-  std::vector<ptgs_light_triangle> ltris;
-  std::vector<ptgs_light_cdf> lcdf;
-  std::vector<ptgs_punctual_light> plights;
-  std::vector<ptgs_punctual_cdf> pcdf;
-};
 
-static ptgs_material default_material() {
+ptgs_material ptgs_default_material() {
   ptgs_material m;
   std::memset(&m, 0, sizeof(m));
   // Material defaults, GeneralHeaders.h:202-235
@@ -258,9 +157,8 @@ int ptgs_builder_add_rtbox_json(ptgs_scene_builder* b, const char* path) {
   std::stringstream ss;
   ss << f.rdbuf();
   std::string text = ss.str();
-  JParser jp{text.data(), text.data() + text.size()};
-  JVal cfg = jp.parse();
-  if (!jp.ok || cfg.kind != JVal::OBJ) { b->err = std::string("bad JSON in ") + path; return PTGS_EIO; }
+  JVal cfg;
+  if (!ptgs::parse_json(text.data(), text.size(), cfg) || cfg.kind != JVal::OBJ) { b->err = std::string("bad JSON in ") + path; return PTGS_EIO; }
   const JVal* jpos = cfg.get("position");
   const JVal* jdim = cfg.get("dimensions");
   const JVal* jpanels = cfg.get("panels");
@@ -300,7 +198,7 @@ int ptgs_builder_add_rtbox_json(ptgs_scene_builder* b, const char* path) {
     const JVal* jm = panel ? panel->get("material") : nullptr;
     const JVal* bc = jm ? jm->get("base_color") : nullptr;
     if (!bc || bc->arr.size() < 3) { b->err = std::string("panel ") + names[i] + " lacks material.base_color"; return PTGS_EIO; }
-    ptgs_material m = default_material();
+    ptgs_material m = ptgs_default_material();
     float c0 = (float)bc->arr[0].num, c1 = (float)bc->arr[1].num, c2 = (float)bc->arr[2].num;
     m.base_color_factor[0] = c0; m.base_color_factor[1] = c1; m.base_color_factor[2] = c2; m.base_color_factor[3] = 1.0f;
     m.metallic_factor = jnum(jm->get("metallic"), 0.0f);
@@ -328,6 +226,10 @@ int ptgs_builder_add_rtbox_json(ptgs_scene_builder* b, const char* path) {
     o.etris.push_back({i0, i1, i2, mi, 0.5f * length(cross(sub(p1, p0), sub(p2, p0)))});
   }
   o.num_textures = 1;
+  // the rt-box's only texture: a 1x1 (125, 125, 125, 255) sRGB default (engine.cpp:331-333)
+  ptgs_scene_builder::Texture gray;
+  gray.rgba = {125, 125, 125, 255};
+  o.textures.push_back(gray);
   b->rtbox = o;
   b->has_rtbox = true;
   return PTGS_OK;
@@ -369,8 +271,15 @@ int ptgs_builder_add_object(ptgs_scene_builder* b, const ptgs_vertex* vertices, 
 int ptgs_builder_finalize(ptgs_scene_builder* b, ptgs_scene_desc* desc, ptgs_ubo* ubo) {
   if (!b || !desc || !ubo) return PTGS_EINVAL;
   b->v.clear(); b->idx.clear(); b->meshes.clear(); b->mesh_count.clear(); b->mats.clear();
-  b->ltris.clear(); b->lcdf.clear(); b->plights.clear(); b->pcdf.clear();
+  b->ltris.clear(); b->lcdf.clear(); b->plights.clear(); b->pcdf.clear(); b->tex.clear();
   std::vector<float> tri_flux;
+  // Texture pixels are emitted (desc->textures) once any object carries decoded images (glTF
+  // ingest); objects added without pixel data then contribute 1x1 white placeholders.
+  bool emit_tex = false;
+  for (const auto& o : b->objects) emit_tex |= !o.textures.empty();
+  static const uint8_t white[4] = {255, 255, 255, 255};
+  // loadScene pushes the scene "sun" before any object light (engine.cpp:1193, :1225-1242)
+  b->plights = b->global_lights;
   int tex_offset = 0;
   auto aggregate = [&](const ptgs_scene_builder::Object& o) {
     if (o.vertices.empty()) return;
@@ -401,6 +310,18 @@ int ptgs_builder_finalize(ptgs_scene_builder* b, ptgs_scene_desc* desc, ptgs_ubo
     }
     for (const ptgs_punctual_light& l : o.lights)
       if (l.intensity > 0.0f) b->plights.push_back(l);
+    if (emit_tex) {
+      for (uint32_t t = 0; t < o.num_textures; ++t) {
+        ptgs_texture d{};
+        if (t < o.textures.size()) {
+          d.rgba8 = o.textures[t].rgba.data(); d.width = o.textures[t].w; d.height = o.textures[t].h;
+          d.srgb = o.textures[t].srgb;
+        } else {
+          d.rgba8 = white; d.width = 1; d.height = 1; d.srgb = 1;
+        }
+        b->tex.push_back(d);
+      }
+    }
     tex_offset += (int)o.num_textures;
   };
   for (const auto& o : b->objects) aggregate(o);
@@ -472,6 +393,8 @@ int ptgs_builder_finalize(ptgs_scene_builder* b, ptgs_scene_desc* desc, ptgs_ubo
   desc->num_punctual_lights = (uint32_t)b->plights.size();
   desc->punctual_cdf = b->pcdf.data();
   desc->num_punctual_cdf = (uint32_t)b->pcdf.size();
+  desc->textures = b->tex.empty() ? nullptr : b->tex.data();
+  desc->num_textures = (uint32_t)b->tex.size();
   return PTGS_OK;
 }
 

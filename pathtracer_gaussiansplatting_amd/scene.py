@@ -186,6 +186,33 @@ class SceneBuilder:
         _abi.check(rc, "ptgs_builder_add_object", self._err())
         return self
 
+    def add_gltf(self, path: str, position=None, rotation_deg=None, scale=None,
+                 missing_images_white: bool = False) -> "SceneBuilder":
+        """One glTF / GLB model (Gameobject::loadModel) placed as a scene-JSON object entry."""
+        def v3(x):
+            return None if x is None else (C.c_float * 3)(*[float(t) for t in x])
+        flags = _abi.INGEST_MISSING_IMAGES_WHITE if missing_images_white else 0
+        rc = _lib().ptgs_builder_add_gltf(self._h, path.encode(), v3(position), v3(rotation_deg), v3(scale), flags)
+        _abi.check(rc, "ptgs_builder_add_gltf", self._err())
+        return self
+
+    def add_punctual_light(self, light) -> "SceneBuilder":
+        """A scene-level light (the settings "sun"): PUNCTUAL_LIGHT_DTYPE record."""
+        lt = np.ascontiguousarray(np.asarray(light, PUNCTUAL_LIGHT_DTYPE).reshape(1))
+        _abi.check(_lib().ptgs_builder_add_punctual_light(self._h, lt.ctypes.data), "ptgs_builder_add_punctual_light",
+                   self._err())
+        return self
+
+    def load_scene_json(self, path: str, root_dir: str | None = None,
+                        missing_images_white: bool = False) -> _abi.SceneSettings:
+        """Engine::loadScene: every object of the scene JSON (+ rt-box); returns the settings."""
+        st = _abi.SceneSettings()
+        flags = _abi.INGEST_MISSING_IMAGES_WHITE if missing_images_white else 0
+        rc = _lib().ptgs_builder_load_scene_json(self._h, path.encode(), None if root_dir is None else root_dir.encode(),
+                                                 flags, C.byref(st))
+        _abi.check(rc, "ptgs_builder_load_scene_json", self._err())
+        return st
+
     def finalize(self) -> Scene:
         d = _abi.SceneDesc()
         ubo = Ubo()
@@ -198,6 +225,13 @@ class SceneBuilder:
             buf = (C.c_char * (n * dt.itemsize)).from_address(ptr)
             return np.frombuffer(bytes(buf), dtype=dt).copy()
 
+        textures = []
+        if d.num_textures:
+            tex = (_abi.Texture * d.num_textures).from_address(d.textures)
+            for t in tex:
+                px = arr(t.rgba8, t.width * t.height * 4, np.dtype(np.uint8)).reshape(t.height, t.width, 4)
+                textures.append((px, bool(t.srgb)))
+
         return Scene(
             vertices=arr(d.vertices, d.num_vertices, VERTEX_DTYPE),
             indices=arr(d.indices, d.num_indices, np.dtype("<u4")),
@@ -209,7 +243,7 @@ class SceneBuilder:
             punctual_lights=arr(d.punctual_lights, d.num_punctual_lights, PUNCTUAL_LIGHT_DTYPE),
             punctual_cdf=arr(d.punctual_cdf, d.num_punctual_cdf, PUNCTUAL_CDF_DTYPE),
             emissive_flux=ubo.emissive_flux, punctual_flux=ubo.punctual_flux, total_flux=ubo.total_flux,
-            p_emissive=ubo.p_emissive)
+            p_emissive=ubo.p_emissive, textures=textures)
 
 
 def make_ubo(pose: CameraPose, scene: Scene, frame_count: int, ambient=(0.0, 0.0, 0.0, 1.0),
@@ -239,3 +273,15 @@ def cornell_box_scene() -> Scene:
 
 def new_hitdata(n: int) -> np.ndarray:
     return np.zeros(n, HITDATA_DTYPE)
+
+
+def decode_image(data: bytes) -> np.ndarray:
+    """PNG / JPEG bytes -> (H, W, 4) uint8 with stbi_load(..., STBI_rgb_alpha) semantics."""
+    lib = _lib()
+    w, h, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    _abi.check(lib.ptgs_image_decode_rgba8(data, len(data), None, 0, C.byref(w), C.byref(h), C.byref(c)),
+               "ptgs_image_decode_rgba8")
+    out = np.empty((h.value, w.value, 4), np.uint8)
+    _abi.check(lib.ptgs_image_decode_rgba8(data, len(data), out.ctypes.data, out.nbytes, C.byref(w), C.byref(h),
+                                           C.byref(c)), "ptgs_image_decode_rgba8")
+    return out
