@@ -176,7 +176,7 @@ def test_ingested_scene_json(renderer, oracle_lib):
     st = b.load_scene_json("main_scene.json", root_dir=fix)
     sc = b.finalize()
     sc.blue_noise = U.blue_noise()
-    assert len(sc.textures) > 10 and sc.num_triangles > 80
+    assert len(sc.textures) > 10 and sc.num_triangles > 60
     W, H = 160, 120
     pose = Camera(aspect=W / H).look_at([0.0, 0.2, 4.3], [0.2, -1.2, 0.0])
     ubo = make_ubo(pose, sc, 0, ambient=tuple(st.ambient_light), height=H, use_lod=st.use_lod,
