@@ -339,6 +339,18 @@ int ptgs_splat_gaussians_over(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs
                               uint32_t tile_row_begin, uint32_t tile_row_end, float* out_rgba32f,
                               ptgs_splat_stats* stats, void* hip_stream);
 
+/* 3DGS initialisation from a point cloud (Kerbl et al. 2023 create_from_pcd; the point cloud is the
+ * reference's points3d.ply, Engine::savePly engine.cpp:2849-2895, read with ptgs_read_ply).
+ * ptgs_knn3_mean_dist2: dist2[i] = mean of the 3 smallest squared distances from point i to the
+ * other points, exact in f32 ((dx*dx + dy*dy) + dz*dz, no FMA; ((b0 + b1) + b2) / 3); fewer than 3
+ * other points: mean of those, none: 0. ptgs_gaussians_from_points writes post-activation
+ * parameters (ptgs_gaussians layout): means = xyz, scales = sqrt(max(dist2, 1e-7)) x3, rotations =
+ * (1, 0, 0, 0), opacities = 0.1, colors = rgb / 255 (rgb: device uchar[3N] or NULL = black).
+ * All buffers are device pointers; both calls synchronise the stream (temporaries are freed). */
+int ptgs_knn3_mean_dist2(ptgs_ctx* ctx, const float* xyz, uint32_t n, float* dist2, void* hip_stream);
+int ptgs_gaussians_from_points(ptgs_ctx* ctx, const float* xyz, const uint8_t* rgb, uint32_t n, float* means,
+                               float* scales, float* rotations, float* opacities, float* colors, void* hip_stream);
+
 /* Debug/parity access to the integer intermediates of the most recent ptgs_splat_gaussians call
  * (device buffers owned by the context, valid until the next splat call):
  * radii[N] (int32), tiles_touched[N] (u32), sorted keys[K] (u64: tile<<32 | depth bits),

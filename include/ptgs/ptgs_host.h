@@ -103,6 +103,13 @@ int ptgs_builder_add_gltf(ptgs_scene_builder* b, const char* path, const float p
  * engine.cpp:1225-1242). */
 int ptgs_builder_add_punctual_light(ptgs_scene_builder* b, const ptgs_punctual_light* light);
 
+/* Vertex element of a PLY point cloud: the ASCII file Engine::savePly writes (engine.cpp:2849-2895,
+ * x y z nx ny nz red green blue) or binary little / big endian. x y z required; normals default 0;
+ * colours from red green blue (uchar, or float in [0,1]) or, failing those, the SH DC term
+ * f_dc_0..2 of a trained 3DGS file, else 0. Pass xyz = normals = rgb = NULL to get the count;
+ * PTGS_ERANGE when capacity < count. Any output pointer may be NULL. */
+int ptgs_read_ply(const char* path, float* xyz, float* normals, uint8_t* rgb, uint32_t capacity, uint32_t* count);
+
 /* Engine::loadScene settings (engine.cpp:1190-1255) with the Engine defaults for absent keys */
 typedef struct ptgs_scene_settings {
     float ambient_light[4];      /* default (0, 0, 0, 1) */

@@ -60,6 +60,8 @@ def lib() -> C.CDLL:
                                              _P]
         L.oracle_free.restype = None
         L.oracle_free.argtypes = [_P]
+        L.oracle_knn3_mean_dist2.restype = None
+        L.oracle_knn3_mean_dist2.argtypes = [_P, _U, _P]
         L.oracle_sincos.restype = None
         L.oracle_sincos.argtypes = [C.c_float, _FP, _FP]
         L.oracle_exp2.restype = C.c_float
@@ -158,3 +160,24 @@ def splat_gaussians(g: dict, ubo, width, height, bg=(0.0, 0.0, 0.0), tile_rows=N
     lib().oracle_free(C.cast(vp, C.c_void_p))
     return {"radii": radii, "touched": touched, "means2d": means2d, "depths": depths, "conic": conic,
             "keys": keys, "vals": vals, "ranges": ranges, "image": image, "K": K}
+
+
+def knn3_mean_dist2(xyz: np.ndarray) -> np.ndarray:
+    """Brute-force 3-NN mean squared distance (the distCUDA2 term of 3DGS initialisation)."""
+    p = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+    out = np.zeros(len(p), np.float32)
+    lib().oracle_knn3_mean_dist2(p.ctypes.data, len(p), out.ctypes.data)
+    return out
+
+
+def gaussians_from_points(xyz: np.ndarray, rgb: np.ndarray | None) -> dict:
+    """create_from_pcd in post-activation form (means, scales, rotations, opacities, colors)."""
+    p = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+    n = len(p)
+    s = np.sqrt(np.maximum(knn3_mean_dist2(p), np.float32(1e-7))).astype(np.float32)
+    rot = np.zeros((n, 4), np.float32)
+    rot[:, 0] = 1.0
+    col = (np.zeros((n, 3), np.float32) if rgb is None
+           else (np.asarray(rgb, np.uint8).reshape(-1, 3).astype(np.float32) / np.float32(255.0)))
+    return {"means": p.copy(), "scales": np.repeat(s[:, None], 3, 1), "rotations": rot,
+            "opacities": np.full(n, 0.1, np.float32), "colors": col}

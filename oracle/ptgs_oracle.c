@@ -1613,6 +1613,34 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
     return (int)K;
 }
 
+/* ---------------------------------------------------------------------------------------------
+ * 3DGS initialisation (Kerbl et al. 2023 create_from_pcd; the distCUDA2 3-NN term): brute force
+ * over all pairs, O(N^2) — the checker for ptgs_knn3_mean_dist2 at small N. Same f32 expressions:
+ * d = (dx*dx + dy*dy) + dz*dz, mean = ((b0 + b1) + b2) / 3; < 3 other points: mean of those; none: 0.
+ * --------------------------------------------------------------------------------------------- */
+void oracle_knn3_mean_dist2(const float* xyz, uint32_t n, float* dist2) {
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    float b0 = INFINITY, b1 = INFINITY, b2 = INFINITY;
+    const float qx = xyz[3 * i], qy = xyz[3 * i + 1], qz = xyz[3 * i + 2];
+    for (uint32_t j = 0; j < n; ++j) {
+      if ((int64_t)j == i) continue;
+      const float dx = xyz[3 * j] - qx, dy = xyz[3 * j + 1] - qy, dz = xyz[3 * j + 2] - qz;
+      const float d = (dx * dx + dy * dy) + dz * dz;
+      if (d < b2) {
+        if (d < b1) {
+          b2 = b1;
+          if (d < b0) { b1 = b0; b0 = d; } else b1 = d;
+        } else {
+          b2 = d;
+        }
+      }
+    }
+    const uint32_t k = n - 1 < 3 ? n - 1 : 3;
+    dist2[i] = k == 3 ? ((b0 + b1) + b2) / 3.0f : k == 2 ? (b0 + b1) / 2.0f : k == 1 ? b0 : 0.0f;
+  }
+}
+
 void oracle_free(void* p) { free(p); }
 
 /* exposes the math primitives for unit tests */

@@ -177,6 +177,8 @@ SYMBOLS = {
     "ptgs_splat_gaussians_over": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _P, _P, _U, _U, _P,
                                        C.POINTER(SplatStats), _P]),
     "ptgs_splat_get_buffers": (_I, [_P, C.POINTER(SplatBuffers)]),
+    "ptgs_knn3_mean_dist2": (_I, [_P, _P, _U, _P, _P]),
+    "ptgs_gaussians_from_points": (_I, [_P, _P, _P, _U, _P, _P, _P, _P, _P, _P]),
     "ptgs_comm_unique_id": (_I, [_P]),
     "ptgs_comm_create": (_I, [_P, _P, C.c_int, C.c_int]),
     "ptgs_comm_destroy": (_I, [_P]),
@@ -208,6 +210,7 @@ SYMBOLS = {
     "ptgs_builder_finalize": (_I, [_P, C.POINTER(SceneDesc), C.POINTER(Ubo)]),
     "ptgs_builder_last_error": (C.c_char_p, [_P]),
     "ptgs_image_decode_rgba8": (_I, [_P, C.c_size_t, _P, C.c_size_t, C.POINTER(_U), C.POINTER(_U), C.POINTER(_U)]),
+    "ptgs_read_ply": (_I, [C.c_char_p, _P, _P, _P, _U, C.POINTER(_U)]),
     "ptgs_builder_add_gltf": (_I, [_P, C.c_char_p, _FP, _FP, _FP, _U]),
     "ptgs_builder_add_punctual_light": (_I, [_P, _P]),
     "ptgs_builder_load_scene_json": (_I, [_P, C.c_char_p, C.c_char_p, _U, C.POINTER(SceneSettings)]),

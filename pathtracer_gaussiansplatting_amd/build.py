@@ -21,9 +21,9 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libptgs.so")
 
 SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "capture.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp",
-           "pt_kernels.hip", "raster.hip", "splat.hip", "gltf.cpp", "image_decode.cpp"]
+           "pt_kernels.hip", "raster.hip", "splat.hip", "knn.hip", "gltf.cpp", "image_decode.cpp", "ply.cpp"]
 # pure host code (scene ingest): plain g++, no device pass
-HOST_SOURCES = {"gltf.cpp", "image_decode.cpp"}
+HOST_SOURCES = {"gltf.cpp", "image_decode.cpp", "ply.cpp"}
 ARCH = os.environ.get("PTGS_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC]

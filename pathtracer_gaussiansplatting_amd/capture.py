@@ -55,6 +55,22 @@ def write_ply(path: str, hits: np.ndarray, lib=None) -> int:
     return n.value
 
 
+def read_ply(path: str, lib=None):
+    """-> (xyz float32 (N, 3), normals float32 (N, 3), rgb uint8 (N, 3)) of a PLY point cloud."""
+    L = _lib(lib)
+    n = C.c_uint32()
+    rc = L.ptgs_read_ply(path.encode(), None, None, None, 0, C.byref(n))
+    if rc:
+        raise _abi.PtgsError(f"ptgs_read_ply: {rc} ({path})")
+    xyz = np.zeros((n.value, 3), np.float32)
+    nrm = np.zeros((n.value, 3), np.float32)
+    rgb = np.zeros((n.value, 3), np.uint8)
+    rc = L.ptgs_read_ply(path.encode(), xyz.ctypes.data, nrm.ctypes.data, rgb.ctypes.data, n.value, C.byref(n))
+    if rc:
+        raise _abi.PtgsError(f"ptgs_read_ply: {rc} ({path})")
+    return xyz, nrm, rgb
+
+
 def write_jpeg(path: str, pixels: np.ndarray, quality: int = 90, lib=None):
     p = np.ascontiguousarray(pixels, np.uint8)
     comp = 1 if p.ndim == 2 else p.shape[2]

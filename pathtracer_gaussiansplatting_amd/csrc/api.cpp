@@ -19,6 +19,7 @@
 #include "../../include/ptgs/ptgs.h"
 #include "bvh.h"
 #include "bvh_gpu.h"
+#include "knn.h"
 #include "hostmath.h"
 #include "pt_launch.h"
 #include "comm.h"
@@ -539,6 +540,32 @@ int ptgs_encode_srgb8(ptgs_ctx* c, const float* rgba32f, uint32_t w, uint32_t h,
   HIPCHK(c, hipSetDevice(c->device));
   hipError_t e = launch_encode_srgb8(rgba32f, rgba8, w * h, (hipStream_t)stream);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "encode_srgb8: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
+int ptgs_knn3_mean_dist2(ptgs_ctx* c, const float* xyz, uint32_t n, float* dist2, void* stream) {
+  if (!c || (n && (!xyz || !dist2))) return fail(c, PTGS_EINVAL, "null argument");
+  if (n == 0) return PTGS_OK;
+  if (!is_device_ptr(xyz) || !is_device_ptr(dist2)) return fail(c, PTGS_EINVAL, "buffers must be device pointers");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipError_t e = ptgs::knn3_mean_dist2(xyz, n, dist2, (hipStream_t)stream, nullptr);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "knn3_mean_dist2: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
+int ptgs_gaussians_from_points(ptgs_ctx* c, const float* xyz, const uint8_t* rgb, uint32_t n, float* means,
+                               float* scales, float* rotations, float* opacities, float* colors, void* stream) {
+  if (!c || (n && (!xyz || !means || !scales || !rotations || !opacities || !colors)))
+    return fail(c, PTGS_EINVAL, "null argument");
+  if (n == 0) return PTGS_OK;
+  const void* ptrs[] = {xyz, means, scales, rotations, opacities, colors};
+  for (const void* p : ptrs)
+    if (!is_device_ptr(p)) return fail(c, PTGS_EINVAL, "buffers must be device pointers");
+  if (rgb && !is_device_ptr(rgb)) return fail(c, PTGS_EINVAL, "buffers must be device pointers");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipError_t e = ptgs::gaussians_from_points(xyz, rgb, n, means, scales, rotations, opacities, colors,
+                                             (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "gaussians_from_points: %s", hipGetErrorString(e));
   return PTGS_OK;
 }
 

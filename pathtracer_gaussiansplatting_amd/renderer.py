@@ -105,6 +105,31 @@ class Renderer:
         rc = self.lib.ptgs_trace_depth(self._h, C.byref(ubo), width, height, _ptr(depth), _stream(stream))
         self._chk(rc, "ptgs_trace_depth")
 
+    # ---------------------------------------------------------------- 3DGS initialisation (§8f #3)
+    def knn3_mean_dist2(self, xyz, dist2, stream=None):
+        """dist2[i] = mean squared distance of point i to its 3 nearest other points (device tensors:
+        xyz float32 [N, 3], dist2 float32 [N])."""
+        n = int(xyz.shape[0])
+        self._chk(self.lib.ptgs_knn3_mean_dist2(self._h, _ptr(xyz), n, _ptr(dist2), _stream(stream)),
+                  "ptgs_knn3_mean_dist2")
+
+    def gaussians_from_points(self, xyz, rgb=None, stream=None) -> dict:
+        """Kerbl et al. create_from_pcd in post-activation form -> dict of device tensors in the
+        splat_gaussians layout (means, scales, rotations, opacities, colors)."""
+        import torch
+        n = int(xyz.shape[0])
+        dev = xyz.device
+        g = {"means": torch.empty((n, 3), dtype=torch.float32, device=dev),
+             "scales": torch.empty((n, 3), dtype=torch.float32, device=dev),
+             "rotations": torch.empty((n, 4), dtype=torch.float32, device=dev),
+             "opacities": torch.empty((n,), dtype=torch.float32, device=dev),
+             "colors": torch.empty((n, 3), dtype=torch.float32, device=dev)}
+        rc = self.lib.ptgs_gaussians_from_points(self._h, _ptr(xyz), _ptr(rgb), n, _ptr(g["means"]), _ptr(g["scales"]),
+                                                 _ptr(g["rotations"]), _ptr(g["opacities"]), _ptr(g["colors"]),
+                                                 _stream(stream))
+        self._chk(rc, "ptgs_gaussians_from_points")
+        return g
+
     # ---------------------------------------------------------------- RCCL frame reduce (§8e)
     def comm_unique_id(self) -> bytes:
         buf = (C.c_uint8 * 128)()
