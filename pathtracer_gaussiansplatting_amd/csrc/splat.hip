@@ -440,7 +440,9 @@ struct GStage {  // one staged blend record (see gs_preprocess_kernel)
 
 // One 256-work-item workgroup per 16x16 tile (a persistent, software-pipelined variant that loads
 // the next tile's keys during the current one measured slower: static tile assignment loses to the
-// dispatcher's dynamic balancing, 103 vs 72 us at C2).
+// dispatcher's dynamic balancing, 103 vs 72 us at C2; a tile-pair workgroup shading two pixels per
+// lane in packed f32 measured 133 vs 104 us per frame: the per-pixel done / valid bookkeeping of the
+// pair and the strip lists cost more than the packing saved).
 //  sort     the tile's pairs by (depth, gaussian): tiles of <= 256 pairs in registers (one key per
 //           work-item; while the network runs, the blend records of the unsorted keys are already
 //           in flight, the key carries its staging slot in its low 8 bits); larger tiles in LDS
@@ -483,7 +485,8 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
     s_stage[GS_BLOCK].b = make_float4(0.0f, -__builtin_huge_valf(), 0.0f, 0.0f);
     s_stage[GS_BLOCK].c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
-  // quadrant mask of a record's alpha box: bit q = (x half q & 1, y half q >> 1)
+  // quadrant mask of a record's alpha box: bit q = (x half q & 1, y half q >> 1). (An exact
+  // ellipse-vs-block refinement was measured slower on C2: 74 vs 71 us.)
   auto quad_mask = [&](const float4& a, const float4& c) -> uint32_t {
     const float x0 = a.x - c.y, x1 = a.x + c.y, y0 = a.y - c.z, y1 = a.y + c.z;
     const bool xl = x0 <= tx0 + 7.0f && x1 >= tx0, xr = x0 <= tx0 + 15.0f && x1 >= tx0 + 8.0f;
@@ -790,7 +793,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e2 = mark(5))) return e2;
     if (rows > 0) {
       auto k = depth ? gs_sort_blend_kernel<true> : gs_sort_blend_kernel<false>;
-      hipLaunchKernelGGL(k, dim3(cam.grid_x, rows), dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p,
+      const dim3 grid(cam.grid_x, rows);
+      hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p,
                          (unsigned long long*)w->pairs.p, (unsigned long long*)w->keys_out.p,
                          (uint32_t*)w->vals_out.p, (const float4*)w->rec.p, bg[0], bg[1], bg[2],
                          (const uint32_t*)w->total.p, cap, n < (1u << 24) ? 1u : 0u,
