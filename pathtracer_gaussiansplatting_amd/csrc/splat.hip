@@ -228,8 +228,12 @@ __global__ __launch_bounds__(256) void gs_preprocess_kernel(SplatCam cam, PreArg
 //           start[t] + sum_{c' < c} hist[c'][t] + (LDS cursor). Chunk-0 blocks publish the ranges.
 // Order inside a tile's segment depends on LDS atomic order and is fixed by the blend's per-tile sort.
 #define GS_BIN_THREADS 1024
+#ifndef GS_BIN_CHUNKS
 #define GS_BIN_CHUNKS 16
+#endif
+#ifndef GS_BIN_UNROLL
 #define GS_BIN_UNROLL 2
+#endif
 #define GS_BAND_TILES 8192  // max tiles per band (LDS); W <= 131072 px
 #define GS_TILE_SLOTS 256   // fixed key slots per tile (= the register-sort limit)
 
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     uint32_t cap, uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs,
     unsigned long long* __restrict__ tile_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];  // 2 * band_rows * grid_x
-  __shared__ uint32_t s_part[GS_BIN_THREADS];
+  __shared__ uint32_t s_part[GS_BIN_THREADS / 64];
   if (*total > cap) return;
   uint32_t ty0, ty1;
   gs_band(bg, ty0, ty1);
@@ -360,15 +364,20 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
   const uint32_t kb = min(nt, tid * per), ke = min(nt, kb + per);
   uint32_t local = 0;
   for (uint32_t k = kb; k < ke; ++k) local += s_tot[k];
-  s_part[tid] = local;
-  __syncthreads();
-  for (uint32_t off = 1; off < GS_BIN_THREADS; off <<= 1) {
-    const uint32_t v = tid >= off ? s_part[tid - off] : 0u;
-    __syncthreads();
-    s_part[tid] += v;
-    __syncthreads();
+  // wave-level inclusive scan by shuffles, then the wave totals (one barrier instead of a
+  // block-wide Hillis-Steele ladder: 20 barriers measured ~8 us of the kernel)
+  const uint32_t lane = tid & 63u, wv = tid >> 6;
+  uint32_t incl = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += u;
   }
-  uint32_t run = band_off[blockIdx.x] + s_part[tid] - local;
+  if (lane == 63) s_part[wv] = incl;
+  __syncthreads();
+  uint32_t woff = 0;
+  for (uint32_t w = 0; w < wv; ++w) woff += s_part[w];
+  uint32_t run = band_off[blockIdx.x] + woff + incl - local;
   for (uint32_t k = kb; k < ke; ++k) {
     const uint32_t tot = s_tot[k];
     if (c == 0) ranges[t0 + k] = tot ? make_uint2(run, run + tot) : make_uint2(0u, 0u);
@@ -495,9 +504,15 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
            ((uint32_t)(xr && yb) << 3);
   };
   // the tile's slot row is loaded together with its range (no dependent round trip for small tiles)
+#ifdef GS_PROBE_SLOT_N
+  const uint2 range = ranges[tile];
+  const uint32_t n = range.y - range.x;
+  const unsigned long long k_slot = tid < n ? tile_slots[(size_t)tile * GS_TILE_SLOTS + tid] : ~0ull;
+#else
   const unsigned long long k_slot = tile_slots[(size_t)tile * GS_TILE_SLOTS + tid];
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
+#endif
   const bool small = slot_keys && n <= GS_BLOCK;
   const bool in_lds = n <= GS_SORT_CAP;
   // where the scatter put this tile's keys: its slot row (<= GS_TILE_SLOTS) or its pair segment
@@ -550,8 +565,10 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
       s_stage[tid].b = rb;
       s_stage[tid].c = rc;
       s_mask[tid] = (uint8_t)quad_mask(ra, rc);
+#ifndef GS_PROBE_NO_PUBLISH
       keys_out[range.x + tid] = tbits | (key >> 32);
       vals_out[range.x + tid] = (uint32_t)(key >> 8) & 0xFFFFFFu;
+#endif
       my_slot = (uint32_t)key & 0xFFu;
     }
   } else {
