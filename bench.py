@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-pt", action="store_true")
     ap.add_argument("--no-hybrid", action="store_true")
     ap.add_argument("--no-gpu-bvh", action="store_true")
+    ap.add_argument("--no-gs-1m", action="store_true", help="skip the 1M-Gaussian splat and the point-cloud init legs")
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
     ap.add_argument("--hybrid-spp", type=int, default=16)
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented counting pass")
@@ -231,7 +232,7 @@ def main():
         for _ in range(max(args.warmup, 1)):
             r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
         torch.cuda.synchronize()
-        gsteps = max(args.steps, 5)
+        gsteps = max(args.steps, 100)  # ~0.1 ms per frame: enough frames for a stable mean
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -262,6 +263,36 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(b_gs / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "alg_bytes": b_gs},
         }
+        out["gs"]["splat_pairs_per_s"] = round(K * world / (gdt / gsteps) / 1e9, 4)  # (Gaussian, tile) instances, G/s
+        del dg
+        # the same forward at the C4 hybrid's Gaussian count (1M), splat only
+        if world == 1 and not args.no_gs_1m:
+            g1 = {k: torch.from_numpy(v).cuda() for k, v in Y.gaussians_c2(args.hybrid_gaussians, seed=3).items()}
+            for _ in range(2):
+                r.splat_gaussians(g1, gubo, W, H, img, stream=stream)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(gsteps):
+                r.splat_gaussians(g1, gubo, W, H, img, stream=stream)
+            torch.cuda.synchronize()
+            d1 = (time.perf_counter() - t0) / gsteps
+            st1 = r.splat_gaussians(g1, gubo, W, H, img, want_stats=True, stream=stream)
+            out["gs_1m"] = {"workload": f"3DGS forward only: {args.hybrid_gaussians} C2-distributed Gaussians, {W}x{H}",
+                            "value": round(args.hybrid_gaussians / d1 / 1e9, 4), "unit": "Gsplats/s",
+                            "ms_per_step": round(d1 * 1e3, 4), "pairs_K": int(st1.num_rendered)}
+            # 3DGS initialisation from a point cloud of that size (exact 3-NN scales, ptgs_gaussians_from_points)
+            pts = g1["means"]
+            rgbp = torch.randint(0, 256, (pts.shape[0], 3), dtype=torch.uint8, device="cuda")
+            r.gaussians_from_points(pts, rgbp, stream=stream)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                r.gaussians_from_points(pts, rgbp, stream=stream)
+            torch.cuda.synchronize()
+            di = (time.perf_counter() - t0) / 3
+            out["gs_init"] = {"workload": f"3DGS init from a {pts.shape[0]}-point cloud (exact 3-NN scales)",
+                              "ms": round(di * 1e3, 3), "mpoints_per_s": round(pts.shape[0] / di / 1e6, 1)}
+            del g1, pts, rgbp
         if args.no_pt:
             out.update({"value": out["gs"]["value"], "unit": "Gsplats/s", "ms_per_step": out["gs"]["ms_per_step"],
                         "config": {"workload": out["gs"]["workload"]}, "data": "synthetic Gaussians (seeded)"})
