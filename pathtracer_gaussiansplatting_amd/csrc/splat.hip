@@ -54,6 +54,7 @@ struct SplatWorkspace {
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
+  uint32_t lds_keys = 2048;  // large-tile LDS sort capacity: from the largest tile seen two frames back
   hipEvent_t ev[7] = {};
   bool timed = false;
 };
@@ -324,6 +325,10 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(BinGrid bg
   }
   if (lane == 0) {
     *total = carry;
+    // the largest tile of the previous frame's scatter (its atomicMax into total[1]), for the host's
+    // choice of the blend's LDS sort capacity; reset for this frame's scatter
+    __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);
+    total[1] = 0;
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
     *ticket = 0;                                        // ready for the next frame (stream order)
   }
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(BinGrid bg
 // re-runs scatter + blend after growing it when it did not: see splat_gaussians).
 __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, uint32_t n,
-    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ band_off, const uint32_t* __restrict__ total,
+    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ band_off, uint32_t* __restrict__ total,
     uint32_t cap, uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs,
     unsigned long long* __restrict__ tile_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];  // 2 * band_rows * grid_x
@@ -378,6 +383,12 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
   uint32_t woff = 0;
   for (uint32_t w = 0; w < wv; ++w) woff += s_part[w];
   uint32_t run = band_off[blockIdx.x] + woff + incl - local;
+  if (c == 0) {  // largest tile of the band -> total[1] (read back by the next frame's count)
+    uint32_t mx = 0;
+    for (uint32_t k = kb; k < ke; ++k) mx = max(mx, s_tot[k]);
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+    if (lane == 0 && mx) atomicMax(total + 1, mx);
+  }
   for (uint32_t k = kb; k < ke; ++k) {
     const uint32_t tot = s_tot[k];
     if (c == 0) ranges[t0 + k] = tot ? make_uint2(run, run + tot) : make_uint2(0u, 0u);
@@ -441,7 +452,12 @@ __device__ __forceinline__ void bitonic_flip_sort(uint32_t n, Swap swap_if) {
   }
 }
 
-#define GS_SORT_CAP 512
+// LDS arena of the blend: staged records + per-quadrant lists; a large tile's sort uses it (or more,
+// dynamic LDS) for up to lds_keys keys, above that global memory. lds_keys follows the largest tile
+// two frames back (count -> k_host[1]), between GS_SORT_MIN and GS_SORT_MAX.
+#define GS_ARENA_MIN (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)
+#define GS_SORT_MIN 2048
+#define GS_SORT_MAX 8192
 
 struct GStage {  // one staged blend record (see gs_preprocess_kernel)
   float4 a, b, c;
@@ -455,7 +471,7 @@ struct GStage {  // one staged blend record (see gs_preprocess_kernel)
 //  sort     the tile's pairs by (depth, gaussian): tiles of <= 256 pairs in registers (one key per
 //           work-item; while the network runs, the blend records of the unsorted keys are already
 //           in flight, the key carries its staging slot in its low 8 bits); larger tiles in LDS
-//           (global memory above GS_SORT_CAP) with records staged in batches of 256.
+//           (global memory above lds_keys) with records staged in batches of 256.
 //  publish  the sorted keys (tile << 32 | depth) / values (gaussian).
 //  blend    wave w shades the 8x8 quadrant q = w of the tile (x half w & 1, y half w >> 1), one pixel
 //           per lane. Each staged Gaussian's alpha box is tested against the four quadrants; a ballot
@@ -476,12 +492,17 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
                                                                  const unsigned long long* __restrict__ tile_slots,
                                                                  const float* __restrict__ depth_lim,
                                                                  const float4* __restrict__ under,
-                                                                 float4* __restrict__ out) {
-  __shared__ unsigned long long s_key[GS_SORT_CAP];
+                                                                 float4* __restrict__ out, uint32_t lds_keys) {
   // staged records of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads the
   // per-quadrant lists to a multiple of 4
-  __shared__ GStage s_stage[GS_BLOCK + 1];
-  __shared__ __attribute__((aligned(16))) uint32_t s_list[4][GS_BLOCK + 4];  // byte offsets into s_stage
+  // One LDS arena: the staged records and the per-quadrant lists (byte offsets into the records).
+  // The sorts' key arrays alias it (the register network's 64 / 128 exchanges: 256 keys; a large
+  // tile: <= lds_keys keys), which is safe because records and lists are written only after
+  // the sort, behind a barrier; the sorted keys / values are read back from keys_out / vals_out.
+  extern __shared__ __attribute__((aligned(16))) char s_arena[];  // max(GS_ARENA_MIN, 8 * lds_keys) bytes
+  GStage* s_stage = reinterpret_cast<GStage*>(s_arena);
+  uint32_t(*s_list)[GS_BLOCK + 4] = reinterpret_cast<uint32_t(*)[GS_BLOCK + 4]>(s_arena + sizeof(GStage) * (GS_BLOCK + 1));
+  unsigned long long* s_key = reinterpret_cast<unsigned long long*>(s_arena);
   __shared__ uint8_t s_mask[GS_BLOCK];
   __shared__ uint32_t s_qcnt[4][4];  // [wave][quadrant]
   if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
@@ -489,11 +510,6 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
   const uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
   const uint32_t tile = tile_y * cam.grid_x + tile_x;
   const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
-  if (tid == 0) {
-    s_stage[GS_BLOCK].a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    s_stage[GS_BLOCK].b = make_float4(0.0f, -__builtin_huge_valf(), 0.0f, 0.0f);
-    s_stage[GS_BLOCK].c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
   // quadrant mask of a record's alpha box: bit q = (x half q & 1, y half q >> 1). (An exact
   // ellipse-vs-block refinement was measured slower on C2: 74 vs 71 us.)
   auto quad_mask = [&](const float4& a, const float4& c) -> uint32_t {
@@ -514,7 +530,7 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
   const uint32_t n = range.y - range.x;
 #endif
   const bool small = slot_keys && n <= GS_BLOCK;
-  const bool in_lds = n <= GS_SORT_CAP;
+  const bool in_lds = n <= lds_keys;
   // where the scatter put this tile's keys: its slot row (<= GS_TILE_SLOTS) or its pair segment
   unsigned long long* seg = n <= GS_TILE_SLOTS
                                 ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
@@ -560,6 +576,7 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
         const bool swap = (other < key) == (((tid & j) == 0) == ((tid & k) == 0));
         key = swap ? other : key;
       }
+    if (npad >= 128) __syncthreads();  // the last exchange reads are done before records overwrite them
     if (tid < n) {
       s_stage[tid].a = ra;
       s_stage[tid].b = rb;
@@ -575,10 +592,12 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
     if (in_lds) {
       for (uint32_t k = tid; k < n; k += GS_BLOCK) s_key[k] = seg[k];
       __syncthreads();
+#ifndef GS_PROBE_NO_BIGSORT
       bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
         unsigned long long x = s_key[a], y = s_key[b];
         if (y < x) { s_key[a] = y; s_key[b] = x; }
       });
+#endif
     } else {
       bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
         unsigned long long x = seg[a], y = seg[b];
@@ -590,6 +609,12 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
       keys_out[range.x + k] = tbits | (v >> 32);
       vals_out[range.x + k] = (uint32_t)v;
     }
+    __syncthreads();  // sorted keys consumed: the arena becomes records / lists; batches read vals_out
+  }
+  if (tid == 0) {  // the null record (alpha 0) that pads the per-quadrant lists
+    s_stage[GS_BLOCK].a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    s_stage[GS_BLOCK].b = make_float4(0.0f, -__builtin_huge_valf(), 0.0f, 0.0f);
+    s_stage[GS_BLOCK].c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
 
 #ifndef GS_PROBE_NO_BLEND
@@ -614,7 +639,7 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
         m = s_mask[slot];
       }
     } else if (idx < n) {
-      const uint32_t g = (uint32_t)(in_lds ? s_key[idx] : seg[idx]);
+      const uint32_t g = vals_out[range.x + idx];
       const float4 ga = rec[3 * g], gb = rec[3 * g + 1], gc = rec[3 * g + 2];
       s_stage[tid].a = ga;
       s_stage[tid].b = gb;
@@ -749,7 +774,10 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = ensure(w->ticket, 16))) return e;
     if ((e = hipMemset(w->ticket.p, 0, 16))) return e;
   }
-  if ((e = ensure(w->total, 16))) return e;
+  if (!w->total.p) {  // [0] = K, [1] = largest tile of the last scatter (see the count kernel)
+    if ((e = ensure(w->total, 16))) return e;
+    if ((e = hipMemset(w->total.p, 0, 16))) return e;
+  }
   if (!w->k_host) {
     if ((e = hipHostMalloc((void**)&w->k_host, 16, hipHostMallocCoherent | hipHostMallocMapped))) return e;
     if ((e = hipHostGetDevicePointer((void**)&w->k_dev, w->k_host, 0))) return e;
@@ -801,7 +829,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   auto enqueue_tail = [&](uint32_t cap) -> hipError_t {
     hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), 2 * band_lds, s,
                        bgrid, (const ushort4*)w->rect.p, (const float*)w->depths.p, n, (const uint32_t*)w->hist.p,
-                       (const uint32_t*)w->band_off.p, (const uint32_t*)w->total.p, cap, (uint2*)w->ranges.p,
+                       (const uint32_t*)w->band_off.p, (uint32_t*)w->total.p, cap, (uint2*)w->ranges.p,
                        (unsigned long long*)w->pairs.p, (unsigned long long*)w->tile_slots.p);
     hipError_t e2 = hipGetLastError();
     if (e2) return e2;
@@ -811,18 +839,25 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if (rows > 0) {
       auto k = depth ? gs_sort_blend_kernel<true> : gs_sort_blend_kernel<false>;
       const dim3 grid(cam.grid_x, rows);
-      hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p,
+      const size_t lds = std::max((size_t)GS_ARENA_MIN, (size_t)w->lds_keys * 8u);
+      hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), lds, s, cam, (const uint2*)w->ranges.p,
                          (unsigned long long*)w->pairs.p, (unsigned long long*)w->keys_out.p,
                          (uint32_t*)w->vals_out.p, (const float4*)w->rec.p, bg[0], bg[1], bg[2],
                          (const uint32_t*)w->total.p, cap, n < (1u << 24) ? 1u : 0u,
-                         (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out);
+                         (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out,
+                         w->lds_keys);
       if ((e2 = hipGetLastError())) return e2;
     }
     return mark(6);
   };
   if ((e = enqueue_tail(cap_now()))) return e;
   if ((e = hipEventSynchronize(w->k_event))) return e;
-  const uint32_t K = *w->k_host;
+  const uint32_t K = w->k_host[0];
+  {  // the next frame's large-tile LDS sort capacity (k_host[1]: largest tile of an earlier frame)
+    uint32_t want = GS_SORT_MIN;
+    while (want < w->k_host[1] && want < GS_SORT_MAX) want <<= 1;
+    w->lds_keys = want;
+  }
   if (K > cap_now()) {  // did not fit: grow (hipFree/hipMalloc order after the no-op kernels) and re-run
     if ((e = ensure(w->pairs, (size_t)K * 8))) return e;
     if ((e = ensure(w->keys_out, (size_t)K * 8))) return e;
