@@ -6,7 +6,9 @@
 # Outputs under gpurun_out/prof_<tag>/; summarise with profiles/parse_rocprof.py <tag>.
 set -euo pipefail
 TAG=${1:-r01}
-ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline"}
+# only the headline legs (C3 path trace, C2 splat): every dispatch of a kernel is the same workload,
+# so the per-kernel averages are the per-launch figures bench.py reports
+ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-hybrid --no-gs-1m --no-gpu-bvh"}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
