@@ -43,6 +43,17 @@ struct ptgs_ctx {
 
 namespace {
 
+// 4-wide collapse whose worst-case traversal stack fits PTGS_STACK: fan-out 4, else 3, else 2 (a
+// 2-wide "collapse" needs the BVH2 depth, which the builders keep below PTGS_STACK)
+static bool collapse_fit(const std::vector<float>& n2, std::vector<float>& n4, uint32_t& num4, uint32_t& dep4) {
+  for (int fan = 4; fan >= 2; --fan) {
+    uint32_t need = 0;
+    ptgs::collapse_bvh4(n2, n4, num4, need, dep4, fan);
+    if (need < PTGS_STACK) return true;
+  }
+  return false;
+}
+
 int fail(ptgs_ctx* c, int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -255,6 +266,22 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     GpuBvh g;
     float ms = 0.0f;
     hipError_t e = build_bvh_gpu(tris, PTGS_STACK - 1, g, &ms);
+    if (e == hipSuccess) {  // 4-wide collapse on the host (D2H of the BVH2 nodes, collapse, H2D)
+      auto t0 = std::chrono::steady_clock::now();
+      std::vector<float> n2((size_t)g.num_nodes * 16), n4;
+      uint32_t num4 = 0, dep4 = 0;
+      if ((e = hipMemcpy(n2.data(), g.nodes, n2.size() * 4, hipMemcpyDeviceToHost)) == hipSuccess) {
+        (void)hipFree(g.nodes);
+        g.nodes = nullptr;
+        if (!collapse_fit(n2, n4, num4, dep4) || hipMalloc(&g.nodes, n4.size() * 4) != hipSuccess ||
+            hipMemcpy(g.nodes, n4.data(), n4.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+          e = hipErrorNotSupported;
+        g.num_nodes = num4;
+        g.depth = dep4;
+      }
+      auto t1 = std::chrono::steady_clock::now();
+      ms += (float)std::chrono::duration<double, std::milli>(t1 - t0).count();  // build_ms includes it
+    }
     if (e == hipSuccess) {
       for (void* p : {(void*)g.nodes, (void*)g.tris, (void*)g.tri_flags}) c->scene_allocs.push_back(p);
       s.nodes = g.nodes;
@@ -264,7 +291,7 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
       c->info.bvh_depth = g.depth;
       c->info.max_leaf_size = 4;
       c->info.build_ms = ms;
-      c->info.device_bytes += (size_t)g.num_nodes * 64 + tris.size() * 52;
+      c->info.device_bytes += (size_t)g.num_nodes * 128 + tris.size() * 52;
       built = true;
     } else if (e == hipErrorNotSupported) {
       (void)hipFree(g.nodes);
@@ -280,7 +307,15 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     build_bvh(tris, 4, PTGS_STACK - 1, bvh);
     auto t1 = std::chrono::steady_clock::now();
     if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
-    if ((rc = upload(c, (const float4*)bvh.nodes.data(), bvh.nodes.size() / 4, &s.nodes))) return rc;
+    {
+      std::vector<float> n4;
+      uint32_t num4 = 0, dep4 = 0;
+      if (!collapse_fit(bvh.nodes, n4, num4, dep4))
+        return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
+      if ((rc = upload(c, (const float4*)n4.data(), n4.size() / 4, &s.nodes))) return rc;
+      bvh.num_nodes = num4;
+      bvh.depth = dep4;
+    }
     if ((rc = upload(c, (const float4*)bvh.tris.data(), bvh.tris.size() / 4, &s.tris))) return rc;
     if ((rc = upload(c, bvh.tri_flags.data(), bvh.tri_flags.size(), &s.tri_flags))) return rc;
     c->info.num_bvh_nodes = bvh.num_nodes;

@@ -219,4 +219,90 @@ void build_bvh(const std::vector<BuildTri>& tris, int max_leaf_size, uint32_t ma
   }
 }
 
+namespace {
+struct Ent4 {
+  float lo[3], hi[3];
+  int32_t ref;
+};
+void bvh2_children(const float* n, Ent4 e[2]) {
+  int32_t c0, c1;
+  std::memcpy(&c0, &n[12], 4);
+  std::memcpy(&c1, &n[13], 4);
+  e[0] = Ent4{{n[0], n[2], n[8]}, {n[1], n[3], n[9]}, c0};
+  e[1] = Ent4{{n[4], n[6], n[10]}, {n[5], n[7], n[11]}, c1};
+}
+float ent_area(const Ent4& e) {
+  float d[3];
+  for (int a = 0; a < 3; ++a) d[a] = std::max(0.0f, e.hi[a] - e.lo[a]);
+  return d[0] * d[1] + d[1] * d[2] + d[2] * d[0];
+}
+}  // namespace
+
+void collapse_bvh4(const std::vector<float>& n2, std::vector<float>& n4, uint32_t& num4, uint32_t& max_stack,
+                   uint32_t& depth4, int max_children) {
+  n4.clear();
+  std::vector<std::pair<int32_t, uint32_t>> queue;  // (BVH2 node, BVH4 slot), breadth first
+  std::vector<std::vector<uint32_t>> kids;          // interior BVH4 children per node
+  std::vector<uint32_t> ncount;                     // non-empty children per node
+  queue.push_back({0, 0u});
+  n4.assign(32, 0.0f);
+  kids.emplace_back();
+  ncount.push_back(0);
+  for (size_t q = 0; q < queue.size(); ++q) {
+    const int32_t b2 = queue[q].first;
+    const uint32_t slot = queue[q].second;
+    Ent4 list[4];
+    int cnt = 2;
+    bvh2_children(&n2[16 * (size_t)b2], list);
+    while (cnt < max_children) {
+      int best = -1;
+      float ba = -1.0f;
+      for (int k = 0; k < cnt; ++k)
+        if (list[k].ref >= 0 && ent_area(list[k]) > ba) { ba = ent_area(list[k]); best = k; }
+      if (best < 0) break;
+      Ent4 sub[2];
+      bvh2_children(&n2[16 * (size_t)list[best].ref], sub);
+      list[best] = sub[0];
+      list[cnt++] = sub[1];
+    }
+    float* f = &n4[32 * (size_t)slot];
+    for (int j = 0; j < 4; ++j) {
+      int32_t child = 0;
+      if (j < cnt) {
+        for (int a = 0; a < 3; ++a) {
+          f[(2 * a) * 4 + j] = list[j].lo[a];
+          f[(2 * a + 1) * 4 + j] = list[j].hi[a];
+        }
+        if (list[j].ref >= 0) {
+          const uint32_t ni = (uint32_t)(n4.size() / 32);
+          n4.resize(n4.size() + 32, 0.0f);
+          f = &n4[32 * (size_t)slot];  // (resize may move the storage)
+          queue.push_back({list[j].ref, ni});
+          kids.emplace_back();
+          ncount.push_back(0);
+          kids[slot].push_back(ni);
+          child = (int32_t)ni;
+        } else {
+          child = list[j].ref;
+        }
+      } else {
+        for (int a = 0; a < 6; ++a) f[a * 4 + j] = 1e30f;  // empty: a point box no ray reaches
+      }
+      std::memcpy(&f[24 + j], &child, 4);
+    }
+    ncount[slot] = (uint32_t)cnt;
+  }
+  num4 = (uint32_t)(n4.size() / 32);
+  // stack need and depth, children after parents (breadth-first order): reverse pass
+  std::vector<uint32_t> need(num4, 0), dep(num4, 1);
+  for (size_t i = num4; i-- > 0;) {
+    uint32_t m = 0, d = 0;
+    for (uint32_t k : kids[i]) { m = std::max(m, need[k]); d = std::max(d, dep[k]); }
+    need[i] = (ncount[i] - 1) + m;
+    dep[i] = 1 + d;
+  }
+  max_stack = need[0];
+  depth4 = dep[0];
+}
+
 }  // namespace ptgs

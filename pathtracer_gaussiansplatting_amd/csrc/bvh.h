@@ -35,4 +35,13 @@ struct BvhOut {
 // max_leaf_size <= 16; the tree depth is bounded by max_depth (>= log2(n / max_leaf_size) + 2)
 void build_bvh(const std::vector<BuildTri>& tris, int max_leaf_size, uint32_t max_depth, BvhOut& out);
 
+// 4-wide collapse of a BVH2 (the layout above): each 4-wide node takes the children of a BVH2 node,
+// repeatedly opening its largest-area interior child until it has 4 (leaves keep their encoding).
+// Layout, 128 B per node (8 float4): lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4],
+// child[4] (int bits, as in BVH2), unused. Empty slots are point boxes at 1e30 (every ray misses).
+// max_stack: traversal stack entries the tree can need (sum over a path of children - 1).
+// max_children (2..4) caps the fan-out (callers retry with fewer when max_stack would not fit).
+void collapse_bvh4(const std::vector<float>& nodes2, std::vector<float>& nodes4, uint32_t& num_nodes4,
+                   uint32_t& max_stack, uint32_t& depth4, int max_children = 4);
+
 }  // namespace ptgs

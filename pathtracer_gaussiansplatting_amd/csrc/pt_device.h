@@ -69,10 +69,11 @@ struct TraversalCounters {
 
 // Traversal stack: PTGS_STACK entries per work-item in LDS, interleaved across the 256 work-items
 // of a workgroup (entry k of lane t at [k * 256 + t]: conflict-free ds_read/ds_write_b32).
-// 32 x 256 x 4 B = 32 KiB per workgroup (4 workgroups = 16 waves per CU fit the 160 KiB LDS); the
-// BVH builder bounds the tree depth below PTGS_STACK.
+// 40 x 256 x 4 B = 40 KiB per workgroup (4 workgroups = 16 waves per CU fill the 160 KiB LDS). A
+// 4-wide node pushes up to 3 entries: the collapse (api.cpp) caps the fan-out until the tree's
+// worst-case stack need fits (4-wide, else 3-, else 2-wide, which the builder's depth bound fits).
 #ifndef PTGS_STACK
-#define PTGS_STACK 32
+#define PTGS_STACK 40
 #endif
 #define PTGS_BLOCK 256
 
@@ -118,36 +119,6 @@ __device__ __forceinline__ Ray make_ray(v3 o, v3 d, float tmin, float tmax) {
   r.inv = mk3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   r.oinv = mk3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
   return r;
-}
-
-// Slab test on the two child boxes of one node. Boxes are padded on the host (bvh.cpp) so the
-// test is conservative w.r.t. the triangle test's rounding.
-__device__ __forceinline__ void box2(const Ray& r, float4 n0, float4 n1, float4 n2, float tcap,
-                                     bool& h0, bool& h1, float& t0, float& t1) {
-#ifdef PTGS_BOX_SUBMUL
-  float ax0 = (n0.x - r.o.x) * r.inv.x, ax1 = (n0.y - r.o.x) * r.inv.x;
-  float ay0 = (n0.z - r.o.y) * r.inv.y, ay1 = (n0.w - r.o.y) * r.inv.y;
-  float az0 = (n2.x - r.o.z) * r.inv.z, az1 = (n2.y - r.o.z) * r.inv.z;
-  float bx0 = (n1.x - r.o.x) * r.inv.x, bx1 = (n1.y - r.o.x) * r.inv.x;
-  float by0 = (n1.z - r.o.y) * r.inv.y, by1 = (n1.w - r.o.y) * r.inv.y;
-  float bz0 = (n2.z - r.o.z) * r.inv.z, bz1 = (n2.w - r.o.z) * r.inv.z;
-#else
-  // lo*inv - o*inv as one v_fma_f32 per plane; the host pads every box by >= 4e-7 x the scene's
-  // coordinate scale, which covers the extra rounding of o*inv (<= 6e-8 |o| in space).
-  float ax0 = __builtin_fmaf(n0.x, r.inv.x, -r.oinv.x), ax1 = __builtin_fmaf(n0.y, r.inv.x, -r.oinv.x);
-  float ay0 = __builtin_fmaf(n0.z, r.inv.y, -r.oinv.y), ay1 = __builtin_fmaf(n0.w, r.inv.y, -r.oinv.y);
-  float az0 = __builtin_fmaf(n2.x, r.inv.z, -r.oinv.z), az1 = __builtin_fmaf(n2.y, r.inv.z, -r.oinv.z);
-  float bx0 = __builtin_fmaf(n1.x, r.inv.x, -r.oinv.x), bx1 = __builtin_fmaf(n1.y, r.inv.x, -r.oinv.x);
-  float by0 = __builtin_fmaf(n1.z, r.inv.y, -r.oinv.y), by1 = __builtin_fmaf(n1.w, r.inv.y, -r.oinv.y);
-  float bz0 = __builtin_fmaf(n2.z, r.inv.z, -r.oinv.z), bz1 = __builtin_fmaf(n2.w, r.inv.z, -r.oinv.z);
-#endif
-  float an = fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fmaxf(fminf(az0, az1), r.tmin));
-  float af = fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fminf(fmaxf(az0, az1), tcap));
-  float bn = fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fmaxf(fminf(bz0, bz1), r.tmin));
-  float bf = fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fminf(fmaxf(bz0, bz1), tcap));
-  h0 = an <= af * 1.0000004f;
-  h1 = bn <= bf * 1.0000004f;
-  t0 = an; t1 = bn;
 }
 
 // Moller-Trumbore, double-sided (TriangleFacingCullDisable, engine.cpp:1460). Operation order is
@@ -222,6 +193,45 @@ __device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, i
   }
 }
 
+// 4-wide nodes (bvh.h collapse_bvh4): one 112-B fetch tests four child boxes; hit children are put
+// in near-to-far order by a 5-comparator network, the nearest is entered and the rest pushed
+// farthest first. The slab test is lo * inv - o * inv as one FMA per plane: the host pads every box
+// by >= 4e-7 x the scene's coordinate scale, which covers the extra rounding of o * inv, so the test
+// is conservative w.r.t. the triangle test and the hits do not depend on the tree.
+struct Box4 {
+  float tn[4];
+  int c[4];
+  uint32_t hits;
+};
+__device__ __forceinline__ void box4(const Ray& r, const float4* np, float tcap, Box4& o) {
+  const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
+  const float4 ch = np[6];
+  const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+  const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+  const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+  const float CH[4] = {ch.x, ch.y, ch.z, ch.w};
+  o.hits = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x0 = __builtin_fmaf(LX[j], r.inv.x, -r.oinv.x), x1 = __builtin_fmaf(HX[j], r.inv.x, -r.oinv.x);
+    const float y0 = __builtin_fmaf(LY[j], r.inv.y, -r.oinv.y), y1 = __builtin_fmaf(HY[j], r.inv.y, -r.oinv.y);
+    const float z0 = __builtin_fmaf(LZ[j], r.inv.z, -r.oinv.z), z1 = __builtin_fmaf(HZ[j], r.inv.z, -r.oinv.z);
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), r.tmin));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tcap));
+    const bool h = tn <= tf * 1.0000004f;
+    o.tn[j] = h ? tn : __builtin_huge_valf();
+    o.c[j] = f2i(CH[j]);
+    o.hits += h ? 1u : 0u;
+  }
+}
+__device__ __forceinline__ void cswap4(Box4& b, int i, int j) {
+  const bool sw = b.tn[j] < b.tn[i];
+  const float ti = b.tn[i], tj = b.tn[j];
+  const int ci = b.c[i], cj = b.c[j];
+  b.tn[i] = sw ? tj : ti; b.tn[j] = sw ? ti : tj;
+  b.c[i] = sw ? cj : ci; b.c[j] = sw ? ci : cj;
+}
+
 template <bool STATS, bool TEX>
 __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
                                              TraversalCounters& cnt) {
@@ -230,25 +240,19 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   int node = 0;
   while (true) {
     while (node >= 0) {
-      const float4* np = sc.nodes + 4 * node;
-      float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
-      bool h0, h1; float t0, t1;
-      box2(r, n0, n1, n2, h.t, h0, h1, t0, t1);
-      if (STATS) cnt.nodes += 2;
-      int c0 = f2i(n3.x), c1 = f2i(n3.y);
-      if (h0 && h1) {
-        int near = c0, far = c1;
-        if (t1 < t0) { near = c1; far = c0; }
-        stack[(sp++) * PTGS_BLOCK] = far;
-        node = near;
-      } else if (h0) {
-        node = c0;
-      } else if (h1) {
-        node = c1;
-      } else {
+      Box4 b;
+      box4(r, sc.nodes + 8 * node, h.t, b);
+      if (STATS) cnt.nodes += 4;
+      if (b.hits == 0) {
         if (sp == 0) return h;
         node = stack[(--sp) * PTGS_BLOCK];
+        continue;
       }
+      cswap4(b, 0, 1); cswap4(b, 2, 3); cswap4(b, 0, 2); cswap4(b, 1, 3); cswap4(b, 1, 2);
+      if (b.hits > 3) stack[(sp++) * PTGS_BLOCK] = b.c[3];
+      if (b.hits > 2) stack[(sp++) * PTGS_BLOCK] = b.c[2];
+      if (b.hits > 1) stack[(sp++) * PTGS_BLOCK] = b.c[1];
+      node = b.c[0];
     }
     leaf_closest<STATS, TEX>(sc, r, node, h, seed, cnt);
     if (sp == 0) return h;
@@ -256,7 +260,6 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   }
 }
 
-// any-hit: true if something blocks the segment [tmin, tmax]
 template <bool STATS, bool TEX>
 __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
                                           TraversalCounters& cnt) {
@@ -264,38 +267,37 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
   int node = 0;
   while (true) {
     while (node >= 0) {
-      const float4* np = sc.nodes + 4 * node;
-      float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
-      bool h0, h1; float t0, t1;
-      box2(r, n0, n1, n2, r.tmax, h0, h1, t0, t1);
-      if (STATS) cnt.nodes += 2;
-      int c0 = f2i(n3.x), c1 = f2i(n3.y);
-      if (h0 && h1) {
-        int near = c0, far = c1;
-        if (t1 < t0) { near = c1; far = c0; }
-        stack[(sp++) * PTGS_BLOCK] = far;
-        node = near;
-      } else if (h0) {
-        node = c0;
-      } else if (h1) {
-        node = c1;
-      } else {
+      Box4 b;
+      box4(r, sc.nodes + 8 * node, r.tmax, b);
+      if (STATS) cnt.nodes += 4;
+      // order is irrelevant for an any-hit query: enter the first hit child, push the others
+      int next = -0x7fffffff - 1;
+      bool have = false;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (b.tn[j] != __builtin_huge_valf()) {
+          if (!have) { next = b.c[j]; have = true; }
+          else stack[(sp++) * PTGS_BLOCK] = b.c[j];
+        }
+      if (!have) {
         if (sp == 0) return false;
         node = stack[(--sp) * PTGS_BLOCK];
+        continue;
       }
+      node = next;
     }
     uint32_t L = (uint32_t)(~node);
     uint32_t start = L & 0x07ffffffu;
     uint32_t count = (L >> 27) + 1u;
     for (uint32_t k = 0; k < count; ++k) {
       const float4* tp = sc.tris + 3u * (start + k);
-      float4 a = tp[0], b = tp[1], c = tp[2];
+      float4 a = tp[0], bb = tp[1], c = tp[2];
       if (STATS) cnt.tris++;
       float t, u, v;
-      if (!tri_isect(r, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), t, u, v)) continue;
+      if (!tri_isect(r, mk3(a.x, a.y, a.z), mk3(bb.x, bb.y, bb.z), mk3(c.x, c.y, c.z), t, u, v)) continue;
       if (!(t >= r.tmin && t <= r.tmax)) continue;
       if (sc.has_transparent && (sc.tri_flags[start + k] & 1u)) {
-        if (!anyhit_accept<TEX>(sc, f2u(a.w), f2u(b.w), u, v, seed, f2u(c.w))) continue;
+        if (!anyhit_accept<TEX>(sc, f2u(a.w), f2u(bb.w), u, v, seed, f2u(c.w))) continue;
       }
       return true;
     }
