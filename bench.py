@@ -258,7 +258,7 @@ def main():
             "value": round(N * world / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
             "workload": f"C2 3DGS forward: {N} synthetic Gaussians, {W}x{H}", "pairs_K": int(K),
             "stages_ms": {k: round(float(v), 4) for k, v in
-                          zip(["preprocess", "count", "scatter", "-", "-", "sort_blend"], stages) if k != "-"},
+                          zip(["preprocess+count", "colscan", "scatter", "-", "-", "sort_blend"], stages) if k != "-"},
             "roofline": {"bound": "hbm", "kernel": "whole pipeline", "achieved": round(b_gs / (gms * 1e-3) / 1e9, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(b_gs / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "alg_bytes": b_gs},

@@ -3,13 +3,14 @@
 // The reference has no Gaussian rasterizer; this restates the published forward
 // pass (Kerbl et al., SIGGRAPH 2023) in the reference's camera conventions (glm::lookAt RH view,
 // Vulkan ZO projection with [1][1] negated, camera.cpp:186-187). Four launches per frame:
-//   1. preprocess   one work-item per Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T,
-//                   EWA Sigma' = J W Sigma W^T J^T (+0.3 low-pass), conic, 3-sigma radius, tile rect,
-//                   a 48-B blend record
-//   2. count        (band of tile rows x chunk of Gaussians) workgroups: LDS tile histograms; the last
-//                   workgroup publishes the band offsets and K (to pinned host memory)
-//   3. scatter      same grid: band tile scan + chunk column offsets, then (depth << 32 | gaussian)
-//                   into each touched tile's segment through LDS cursors; tile ranges
+//   1. count        (band of tile rows x chunk of Gaussians) workgroups: preprocess one Gaussian per
+//                   work-item (frustum cull (d <= 0.2), Sigma = R S^2 R^T, EWA Sigma' = J W Sigma W^T J^T
+//                   (+0.3 low-pass), conic, 3-sigma radius, tile rect, a 48-B blend record), then the
+//                   chunk's pairs into an LDS tile histogram (load-balanced wave expansion)
+//   2. colscan      per 64 tiles: prefix of the histograms over the chunks, tile totals, K (to pinned
+//                   host memory)
+//   3. scatter      same grid as 1: (depth << 32 | gaussian) into each touched tile's segment through
+//                   LDS cursors; tile ranges
 //   4. sort+blend   one workgroup per 16x16 tile: sort by (depth, gaussian) (= the order of a stable
 //                   global sort of (tile << 32 | depth) keys), publish keys/values, per-quadrant
 //                   culled front-to-back alpha blend
@@ -48,8 +49,8 @@ struct DevBuf {
 };
 
 struct SplatWorkspace {
-  DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, band_total,
-      band_off, tile_slots, point_keys, total, rect, ticket;
+  DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, tile_info,
+      group_total, tile_slots, point_keys, total, rect;
   uint32_t* k_host = nullptr;  // pinned, coherent: the scan kernel stores K here
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
@@ -64,8 +65,8 @@ SplatWorkspace* splat_workspace_create() { return new SplatWorkspace(); }
 void splat_workspace_destroy(SplatWorkspace* w) {
   if (!w) return;
   DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rec, &w->radii, &w->touched, &w->pairs, &w->keys_out,
-                   &w->vals_out, &w->ranges, &w->hist, &w->band_total, &w->band_off, &w->tile_slots, &w->point_keys,
-                   &w->total, &w->rect, &w->ticket};
+                   &w->vals_out, &w->ranges, &w->hist, &w->tile_info, &w->group_total, &w->tile_slots, &w->point_keys,
+                   &w->total, &w->rect};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
@@ -107,8 +108,10 @@ struct PreArgs {
 };
 
 // One Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T, EWA Sigma' = J W Sigma W^T J^T + 0.3,
-// conic, 3-sigma radius, tile rect, blend record.
-__device__ __forceinline__ void gs_preprocess_one(const SplatCam& cam, const PreArgs& A, uint32_t i) {
+// conic, 3-sigma radius, tile rect (returned; empty if culled) and, with STORE, every per-Gaussian
+// output incl. the blend record. (Blocks of other bands recompute the rect without storing.)
+template <bool STORE>
+__device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const PreArgs& A, uint32_t i) {
   const float* __restrict__ means = A.means;
   const float* __restrict__ scales = A.scales;
   const float* __restrict__ rots = A.rots;
@@ -121,14 +124,17 @@ __device__ __forceinline__ void gs_preprocess_one(const SplatCam& cam, const Pre
   uint32_t* __restrict__ touched = A.touched;
   ushort4* __restrict__ rects = A.rects;
   float4* __restrict__ rec = A.rec;
-  radii[i] = 0;
-  touched[i] = 0;
-  rects[i] = make_ushort4(0, 0, 0, 0);  // empty rect: the scatter reads rects only
+  const ushort4 none = make_ushort4(0, 0, 0, 0);
+  if (STORE) {
+    radii[i] = 0;
+    touched[i] = 0;
+    rects[i] = none;  // empty rect: the scatter reads rects only
+  }
   float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   // frustum: view-space depth d = -z (RH, camera looks down -Z)
   v4 pv = mv4(cam.view, mx, my, mz, 1.0f);
   float d = -pv.z;
-  if (d <= 0.2f) return;
+  if (d <= 0.2f) return none;
   v4 ph = mv4(cam.mvp, mx, my, mz, 1.0f);
   float pw = 1.0f / (ph.w + 0.0000001f);
   float px = ph.x * pw, py = ph.y * pw;
@@ -173,7 +179,7 @@ __device__ __forceinline__ void gs_preprocess_one(const SplatCam& cam, const Pre
   float cc = ((U10 * T10 + U11 * T11) + U12 * T12) + 0.3f;
 
   float det = ca * cc - cb * cb;
-  if (det == 0.0f) return;
+  if (det == 0.0f) return none;
   float det_inv = 1.0f / det;
   float4 con = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, opac[i]);
   float mid = 0.5f * (ca + cc);
@@ -189,14 +195,16 @@ __device__ __forceinline__ void gs_preprocess_one(const SplatCam& cam, const Pre
   rmin_y = max(rmin_y, (int)cam.row_begin);
   rmax_y = min(rmax_y, (int)cam.row_end);
   int area = (rmax_x - rmin_x) * (rmax_y - rmin_y);
-  if (rmax_x <= rmin_x || rmax_y <= rmin_y || area == 0) return;
+  if (rmax_x <= rmin_x || rmax_y <= rmin_y || area == 0) return none;
+  const ushort4 rect = make_ushort4((unsigned short)rmin_x, (unsigned short)rmin_y, (unsigned short)rmax_x,
+                                    (unsigned short)rmax_y);
+  if (!STORE) return rect;
   depths[i] = d;
   radii[i] = r;
   means2d[i] = pimg;
   conic_o[i] = con;
   touched[i] = (uint32_t)area;
-  rects[i] = make_ushort4((unsigned short)rmin_x, (unsigned short)rmin_y, (unsigned short)rmax_x,
-                          (unsigned short)rmax_y);
+  rects[i] = rect;
   // Blend record (3 x float4), the form the blend loop consumes:
   //   (x, y, A, B), (C, log2 o, r, g), (b, ex, ey, depth)  with  A = -a/2 log2e, B = -b log2e, C = -c/2 log2e
   // so that z = A dx^2 + B dx dy + C dy^2 + log2 o = power * log2e + log2 o and alpha = min(0.99, 2^z).
@@ -210,36 +218,32 @@ __device__ __forceinline__ void gs_preprocess_one(const SplatCam& cam, const Pre
   rec[3 * i] = make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E);
   rec[3 * i + 1] = make_float4(-0.5f * con.z * L2E, __log2f(con.w), colors[3 * i], colors[3 * i + 1]);
   rec[3 * i + 2] = make_float4(colors[3 * i + 2], ex, ey, d);
-}
-
-__global__ __launch_bounds__(256) void gs_preprocess_kernel(SplatCam cam, PreArgs A) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < A.n) gs_preprocess_one(cam, A, i);
+  return rect;
 }
 
 // ---- binning --------------------------------------------------------------------------------------
-// No global atomics per pair (contended scattered atomics measured 100 us for C2's 617k pairs):
-// the grid is (bands, chunks): a band is a run of band_rows tile rows, a chunk a contiguous range
-// of Gaussians.
-//  count    block (band, c) counts the pairs of chunk c that fall in its band into an LDS histogram of
-//           the band's tiles (ds_add), writes it to hist[c][t] and adds its total to band_total[band];
-//           the last block to finish (ticket) turns the band totals into band offsets and K.
-//  scatter  block (band, c) recomputes its band's tile starts (band offset + scan of the band's tile
-//           totals) and its chunk's column offsets, then re-walks chunk c and places each pair at
-//           start[t] + sum_{c' < c} hist[c'][t] + (LDS cursor). Chunk-0 blocks publish the ranges.
+// No global atomics per pair (contended scattered atomics measured 100 us for C2's 617k pairs). The
+// grid is (bands, chunks): a band is a run of band_rows tile rows (as many as fit GS_BAND_TILES: the
+// whole 1080p frame is one band, 4K takes 4), a chunk a contiguous range of Gaussians.
+//  count    block (band, c) preprocesses chunk c (band-0 blocks store the per-Gaussian outputs, the
+//           others only recompute the rects) and counts the chunk's pairs in its band into an LDS
+//           histogram (ds_add), written to hist[c][t].
+//  colscan  one block per 64 tiles: hist[c][t] -> exclusive prefix over the chunks (in place), the
+//           tile totals, their exclusive scan inside the 64-tile group and the group totals; K and
+//           the largest tile go to pinned host memory (last block).
+//  scatter  block (band, c): tile starts = scan of the group totals + in-group offset; re-walks chunk
+//           c and places each pair at start[t] + hist[c][t] + (LDS cursor). Chunk-0 blocks publish
+//           the ranges.
 // Order inside a tile's segment depends on LDS atomic order and is fixed by the blend's per-tile sort.
 #define GS_BIN_THREADS 1024
-#ifndef GS_BIN_CHUNKS
-#define GS_BIN_CHUNKS 16
-#endif
-#ifndef GS_BIN_UNROLL
-#define GS_BIN_UNROLL 2
-#endif
-#define GS_BAND_TILES 8192  // max tiles per band (LDS); W <= 131072 px
-#define GS_TILE_SLOTS 256   // fixed key slots per tile (= the register-sort limit)
+#define GS_MAX_CHUNKS 256    // colscan: 4 waves x 64 chunks
+#define GS_CHUNK_MIN 1024    // Gaussians per chunk (at least)
+#define GS_BAND_TILES 8192   // max tiles per band (LDS: 32 KiB count, 64 KiB scatter); W <= 131072 px
+#define GS_TILE_SLOTS 256    // fixed key slots per tile (= the register-sort limit)
+#define GS_MAX_GROUPS 4096   // 64-tile groups (262144 tiles)
 
 struct BinGrid {
-  uint32_t band_rows, bands, chunks, chunk, grid_x, grid_y, tiles;
+  uint32_t band_rows, bands, chunks, chunk, grid_x, grid_y, tiles, groups;
 };
 
 __device__ __forceinline__ void gs_band(const BinGrid& bg, uint32_t& ty0, uint32_t& ty1) {
@@ -247,172 +251,255 @@ __device__ __forceinline__ void gs_band(const BinGrid& bg, uint32_t& ty0, uint32
   ty1 = min(bg.grid_y, ty0 + bg.band_rows);
 }
 
-// walk chunk blockIdx.y's rects, GS_BIN_UNROLL loads in flight per work-item; f(i, rect, y0, y1) for
-// every Gaussian whose rect meets the band rows [ty0, ty1)
-template <typename F>
-__device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* __restrict__ rects, uint32_t n,
-                                              uint32_t ty0, uint32_t ty1, F f) {
-  const uint32_t b0 = blockIdx.y * bg.chunk, b1 = min(n, b0 + bg.chunk);
-  for (uint32_t base = b0 + threadIdx.x; base < b1; base += GS_BIN_THREADS * GS_BIN_UNROLL) {
-    ushort4 rc[GS_BIN_UNROLL];
-#pragma unroll
-    for (int u = 0; u < GS_BIN_UNROLL; ++u) {
-      const uint32_t i = base + u * GS_BIN_THREADS;
-      rc[u] = i < b1 ? rects[i] : make_ushort4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < GS_BIN_UNROLL; ++u) {
-      const uint32_t y0 = max((uint32_t)rc[u].y, ty0), y1 = min((uint32_t)rc[u].w, ty1);
-      if (y0 < y1 && rc[u].x < rc[u].z) f(base + u * GS_BIN_THREADS, rc[u], y0, y1);
-    }
-  }
-}
-
-__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(BinGrid bg, const ushort4* __restrict__ rects,
-                                                                      uint32_t n, uint32_t* __restrict__ hist,
-                                                                      uint32_t* __restrict__ band_total,
-                                                                      uint32_t* __restrict__ band_off,
-                                                                      uint32_t* __restrict__ total,
-                                                                      uint32_t* __restrict__ ticket, uint32_t* k_host) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
-  __shared__ uint32_t s_sum[GS_BIN_THREADS / 64];
-  __shared__ bool s_last;
-  uint32_t ty0, ty1;
-  gs_band(bg, ty0, ty1);
-  const uint32_t nt = (ty1 - ty0) * bg.grid_x;
-  for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) s_hist[k] = 0;
-  __syncthreads();
-#ifndef GS_PROBE_NO_WALK
-  gs_walk_chunk(bg, rects, n, ty0, ty1, [&](uint32_t, const ushort4& rc, uint32_t y0, uint32_t y1) {
-    for (uint32_t y = y0; y < y1; ++y)
-      for (uint32_t x = rc.x; x < rc.z; ++x) atomicAdd(s_hist + (y - ty0) * bg.grid_x + x, 1u);
-  });
-#endif
-  __syncthreads();
-  uint32_t* row = hist + (size_t)blockIdx.y * bg.tiles + ty0 * bg.grid_x;
-  uint32_t part = 0;
-  for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) {
-    const uint32_t c = s_hist[k];
-    row[k] = c;
-    part += c;
-  }
-  for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
-  if ((threadIdx.x & 63u) == 0) s_sum[threadIdx.x >> 6] = part;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t blk = 0;
-    for (int w = 0; w < GS_BIN_THREADS / 64; ++w) blk += s_sum[w];
-    if (blk) atomicAdd(band_total + blockIdx.x, blk);
-    __builtin_amdgcn_s_waitcnt(0);  // the band-total add has been performed before the ticket
-    s_last = atomicAdd(ticket, 1u) == gridDim.x * gridDim.y - 1;
-  }
-  __syncthreads();
-  if (!s_last || threadIdx.x >= 64) return;
-  // last block, wave 0: band offsets (exclusive) and K; the band totals are read by exchange (where
-  // the adds were performed) and re-zeroed for the next frame; 64 bands per step, shuffle scan
-  const uint32_t lane = threadIdx.x;
-  uint32_t carry = 0;
-  for (uint32_t b0 = 0; b0 < bg.bands; b0 += 64) {
-    const uint32_t b = b0 + lane;
-    const uint32_t v = b < bg.bands ? atomicExch(band_total + b, 0u) : 0u;
-    uint32_t incl = v;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t u = __shfl_up(incl, off);
-      if ((int)lane >= off) incl += u;
-    }
-    if (b < bg.bands) band_off[b] = carry + incl - v;
-    carry += __shfl(incl, 63);
-  }
-  if (lane == 0) {
-    *total = carry;
-    // the largest tile of the previous frame's scatter (its atomicMax into total[1]), for the host's
-    // choice of the blend's LDS sort capacity; reset for this frame's scatter
-    __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);
-    total[1] = 0;
-    __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
-    *ticket = 0;                                        // ready for the next frame (stream order)
-  }
-}
-
-// Pairs are written only when K fits the pair buffer (the host sizes it from the previous K and
-// re-runs scatter + blend after growing it when it did not: see splat_gaussians).
-__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
-    BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, uint32_t n,
-    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ band_off, uint32_t* __restrict__ total,
-    uint32_t cap, uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs,
-    unsigned long long* __restrict__ tile_slots) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];  // 2 * band_rows * grid_x
-  __shared__ uint32_t s_part[GS_BIN_THREADS / 64];
-  if (*total > cap) return;
-  uint32_t ty0, ty1;
-  gs_band(bg, ty0, ty1);
-  const uint32_t nt = (ty1 - ty0) * bg.grid_x, t0 = ty0 * bg.grid_x;
-  uint32_t* s_tot = s_cur + nt;
-  const uint32_t c = blockIdx.y, tid = threadIdx.x;
-  // tile totals of the band and this chunk's column offsets
-  for (uint32_t k = tid; k < nt; k += GS_BIN_THREADS) {
-    uint32_t h[GS_BIN_CHUNKS];
-#pragma unroll
-    for (int r = 0; r < GS_BIN_CHUNKS; ++r) h[r] = r < (int)bg.chunks ? hist[(size_t)r * bg.tiles + t0 + k] : 0u;
-    uint32_t col = 0, tot = 0;
-#pragma unroll
-    for (int r = 0; r < GS_BIN_CHUNKS; ++r) {
-      col += r < (int)c ? h[r] : 0u;
-      tot += h[r];
-    }
-    s_cur[k] = col;
-    s_tot[k] = tot;
-  }
-  __syncthreads();
-  // exclusive scan of the band's tile totals: contiguous runs per work-item + Hillis-Steele
-  const uint32_t per = (nt + GS_BIN_THREADS - 1) / GS_BIN_THREADS;
-  const uint32_t kb = min(nt, tid * per), ke = min(nt, kb + per);
-  uint32_t local = 0;
-  for (uint32_t k = kb; k < ke; ++k) local += s_tot[k];
-  // wave-level inclusive scan by shuffles, then the wave totals (one barrier instead of a
-  // block-wide Hillis-Steele ladder: 20 barriers measured ~8 us of the kernel)
-  const uint32_t lane = tid & 63u, wv = tid >> 6;
-  uint32_t incl = local;
+// Pairs of one wave's 64 entries (gaussian g, x0 | w << 16, y0 | h << 16; h = 0: none), walked 64 per
+// step: a shuffle scan of the rect areas; lane q's pair belongs to the first entry whose inclusive
+// sum exceeds q (6-step binary search over shuffles), its tile is (x0 + r % w, y0 + r / w) for its
+// rank r inside that rect. Every lane works on every step but the last (a per-Gaussian rect loop
+// idles the lanes of the smaller rects: C2's rects hold 1 to ~100 tiles). f(g, x, y, depth).
+template <bool WANT_DEPTH, typename F>
+__device__ __forceinline__ void gs_expand(uint32_t lane, uint32_t eg, uint32_t exw, uint32_t eyh, float dep, F f) {
+  const uint32_t a = (exw >> 16) * (eyh >> 16);
+  uint32_t incl = a;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const uint32_t u = __shfl_up(incl, off);
     if ((int)lane >= off) incl += u;
   }
-  if (lane == 63) s_part[wv] = incl;
-  __syncthreads();
-  uint32_t woff = 0;
-  for (uint32_t w = 0; w < wv; ++w) woff += s_part[w];
-  uint32_t run = band_off[blockIdx.x] + woff + incl - local;
-  if (c == 0) {  // largest tile of the band -> total[1] (read back by the next frame's count)
-    uint32_t mx = 0;
-    for (uint32_t k = kb; k < ke; ++k) mx = max(mx, s_tot[k]);
-    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
-    if (lane == 0 && mx) atomicMax(total + 1, mx);
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(incl, 63));
+  const uint32_t excl = incl - a;
+  for (uint32_t p = 0; p < total; p += 64) {
+    const uint32_t qi = p + lane;
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) lo = __shfl(incl, (int)(lo + step - 1)) <= qi ? lo + step : lo;
+    const uint32_t og = __shfl(eg, (int)lo), oxw = __shfl(exw, (int)lo), oy = __shfl(eyh, (int)lo);
+    const uint32_t oex = __shfl(excl, (int)lo);
+    const float od = WANT_DEPTH ? __shfl(dep, (int)lo) : 0.0f;
+    if (qi < total) {
+      const uint32_t r = qi - oex, ow = oxw >> 16;
+      uint32_t row = (uint32_t)((float)r * __builtin_amdgcn_rcpf((float)ow));  // r < 2^13: off by <= 1
+      row = row * ow > r ? row - 1 : row;
+      row = (row + 1) * ow <= r ? row + 1 : row;
+      f(og, (oxw & 0xFFFFu) + (r - row * ow), (oy & 0xFFFFu) + row, od);
+    }
   }
-  for (uint32_t k = kb; k < ke; ++k) {
-    const uint32_t tot = s_tot[k];
-    if (c == 0) ranges[t0 + k] = tot ? make_uint2(run, run + tot) : make_uint2(0u, 0u);
-    // s_cur: this chunk's next slot inside the tile; s_tot -> where the tile's pairs go: its fixed
-    // GS_TILE_SLOTS-slot row when they fit (the blend then loads keys without waiting for the range),
-    // else its segment of the pair buffer (flag bit 31)
-    s_tot[k] = tot <= GS_TILE_SLOTS ? (t0 + k) * GS_TILE_SLOTS : (run | 0x80000000u);
-    run += tot;
+}
+
+__device__ __forceinline__ void gs_clip(const ushort4& rc, uint32_t ty0, uint32_t ty1, uint32_t& xw, uint32_t& yh) {
+  const uint32_t y0 = max((uint32_t)rc.y, ty0), y1 = min((uint32_t)rc.w, ty1);
+  const bool hit = y0 < y1 && rc.x < rc.z;  // culled Gaussians hold the empty rect
+  xw = (uint32_t)rc.x | ((uint32_t)(rc.z - rc.x) << 16);
+  yh = hit ? (y0 | ((y1 - y0) << 16)) : 0u;
+}
+
+// Scatter's walk of chunk blockIdx.y inside the band: with several bands most rects miss the band, so
+// each wave first filters (64 rects per step, GS_WALK_PF steps in flight; ballot + mbcnt append the
+// hits to its GS_WQ-entry LDS ring) and expands 64 queued entries at a time (depths gathered then).
+#define GS_WQ 128
+#define GS_WALK_PF 4
+template <typename F>
+__device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* __restrict__ rects,
+                                              const float* __restrict__ depths, uint32_t n, uint32_t ty0,
+                                              uint32_t ty1, uint4* s_q, F f) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t b0 = blockIdx.y * bg.chunk, b1 = min(n, b0 + bg.chunk);
+  const ushort4 zero = make_ushort4(0, 0, 0, 0);
+  uint4* q = s_q + wave * GS_WQ;
+  uint32_t base = b0 + wave * 64u;
+  ushort4 pf[GS_WALK_PF];
+#pragma unroll
+  for (int k = 0; k < GS_WALK_PF; ++k) {
+    const uint32_t i = base + k * GS_BIN_THREADS + lane;
+    pf[k] = i < b1 ? rects[i] : zero;
+  }
+  uint32_t head = 0, cnt = 0;  // wave-uniform ring state
+  for (;;) {
+    while (cnt < 64u && base < b1) {
+      const ushort4 rc = pf[0];
+#pragma unroll
+      for (int k = 0; k < GS_WALK_PF - 1; ++k) pf[k] = pf[k + 1];
+      {
+        const uint32_t i = base + GS_WALK_PF * GS_BIN_THREADS + lane;
+        pf[GS_WALK_PF - 1] = i < b1 ? rects[i] : zero;
+      }
+      uint32_t xw, yh;
+      gs_clip(rc, ty0, ty1, xw, yh);
+      const unsigned long long bal = __ballot(yh != 0u);
+      if (bal) {
+        if (yh) {
+          const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          q[(head + cnt + pos) & (GS_WQ - 1u)] = make_uint4(base + lane, xw, yh, 0u);
+        }
+        cnt += (uint32_t)__popcll(bal);
+      }
+      base += GS_BIN_THREADS;
+    }
+    if (cnt == 0) break;
+    const uint32_t take = min(64u, cnt);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint4 e = lane < take ? q[(head + lane) & (GS_WQ - 1u)] : make_uint4(0u, 0u, 0u, 0u);
+    head += take;
+    cnt -= take;
+    const float dep = lane < take ? depths[e.x] : 0.0f;
+    gs_expand<true>(lane, e.x, e.y, e.z, dep, f);
+  }
+}
+
+// preprocess + count. Block (0, 0) also hands the previous frame's largest tile (total[1], colscan's
+// atomicMax) to the host (the blend's LDS sort capacity) and re-arms it.
+__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
+                                                                      uint32_t* __restrict__ hist,
+                                                                      uint32_t* __restrict__ total,
+                                                                      uint32_t* k_host) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
+  uint32_t ty0, ty1;
+  gs_band(bg, ty0, ty1);
+  const uint32_t nt = (ty1 - ty0) * bg.grid_x;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) s_hist[k] = 0;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);
+    total[1] = 0;
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t b0 = blockIdx.y * bg.chunk, b1 = min(A.n, b0 + bg.chunk);
+  for (uint32_t base = b0 + wave * 64u; base < b1; base += GS_BIN_THREADS) {
+    const uint32_t i = base + lane;
+    ushort4 rc = make_ushort4(0, 0, 0, 0);
+    if (i < b1) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i) : gs_preprocess_one<false>(cam, A, i);
+#ifndef GS_PROBE_NO_WALK
+    uint32_t xw, yh;
+    gs_clip(rc, ty0, ty1, xw, yh);
+    if (__ballot(yh != 0u))
+      gs_expand<false>(lane, i, xw, yh, 0.0f, [&](uint32_t, uint32_t x, uint32_t y, float) {
+        atomicAdd(s_hist + (y - ty0) * bg.grid_x + x, 1u);
+      });
+#endif
+  }
+  __syncthreads();
+  uint32_t* row = hist + (size_t)blockIdx.y * bg.tiles + ty0 * bg.grid_x;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) row[k] = s_hist[k];
+}
+
+// One 256-work-item block per 64-tile group g: wave w sums chunks [w*cpw, (w+1)*cpw) of the group's
+// 64 tiles (lane = tile: coalesced rows), then rewrites hist[c][t] as the exclusive prefix over c.
+// Outputs per tile (offset inside the group, total), per group its total, and atomicMax of the
+// largest tile into total[1].
+__global__ __launch_bounds__(256) void gs_bin_colscan_kernel(BinGrid bg, uint32_t* __restrict__ hist,
+                                                             uint2* __restrict__ tile_info,
+                                                             uint32_t* __restrict__ group_total,
+                                                             uint32_t* __restrict__ total) {
+  __shared__ uint32_t s_ws[4][64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t t = blockIdx.x * 64u + lane;
+  const bool ok = t < bg.tiles;
+  const uint32_t cpw = (bg.chunks + 3u) / 4u, c0 = wave * cpw, c1 = min(bg.chunks, c0 + cpw);
+  // all of this wave's rows in flight at once (cpw <= 64: registers, fully unrolled)
+  uint32_t h[GS_MAX_CHUNKS / 4];
+  uint32_t sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < GS_MAX_CHUNKS / 4; ++k) {
+    h[k] = (ok && c0 + k < c1) ? hist[(size_t)(c0 + k) * bg.tiles + t] : 0u;
+    sum += h[k];
+  }
+  s_ws[wave][lane] = sum;
+  __syncthreads();
+  uint32_t run = 0;
+  for (uint32_t w = 0; w < wave; ++w) run += s_ws[w][lane];
+#pragma unroll
+  for (uint32_t k = 0; k < GS_MAX_CHUNKS / 4; ++k)
+    if (ok && c0 + k < c1) {
+      hist[(size_t)(c0 + k) * bg.tiles + t] = run;
+      run += h[k];
+    }
+  if (wave != 0) return;
+  const uint32_t tot = s_ws[0][lane] + s_ws[1][lane] + s_ws[2][lane] + s_ws[3][lane];
+  uint32_t incl = tot;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += u;
+  }
+  if (ok) tile_info[t] = make_uint2(incl - tot, tot);  // (offset inside the group, tile total)
+  uint32_t mx = tot;
+  for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+  const uint32_t gsum = __shfl(incl, 63);
+  if (lane == 0) {
+    group_total[blockIdx.x] = gsum;
+    if (mx) atomicMax(total + 1, mx);
+  }
+}
+
+// K = the sum of the group totals (every block scans them all); block (0, 0) publishes it to total[0]
+// (the blend's check) and to pinned host memory. Pairs are written only when K fits the pair buffer
+// (the host sizes it from the previous K and re-runs scatter + blend after growing it when it did
+// not: see splat_gaussians).
+__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
+    BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, uint32_t n,
+    const uint32_t* __restrict__ hist, const uint2* __restrict__ tile_info, const uint32_t* __restrict__ group_total,
+    uint32_t* __restrict__ total, uint32_t* k_host, uint32_t cap, uint2* __restrict__ ranges,
+    unsigned long long* __restrict__ pairs, unsigned long long* __restrict__ tile_slots) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];  // 2 * band_rows * grid_x + groups
+  __shared__ uint4 s_q[GS_BIN_THREADS / 64 * GS_WQ];
+  __shared__ uint32_t s_part[GS_BIN_THREADS / 64];
+  uint32_t ty0, ty1;
+  gs_band(bg, ty0, ty1);
+  const uint32_t nt = (ty1 - ty0) * bg.grid_x, t0 = ty0 * bg.grid_x;
+  uint32_t* s_tot = s_cur + bg.band_rows * bg.grid_x;
+  uint32_t* s_gpre = s_tot + bg.band_rows * bg.grid_x;
+  const uint32_t c = blockIdx.y, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  // exclusive scan of the group totals
+  const uint32_t gend = bg.groups;
+  uint32_t carry = 0;
+  for (uint32_t g0 = 0; g0 < gend; g0 += GS_BIN_THREADS) {
+    const uint32_t g = g0 + tid;
+    const uint32_t v = g < gend ? group_total[g] : 0u;
+    uint32_t incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t u = __shfl_up(incl, off);
+      if ((int)lane >= off) incl += u;
+    }
+    if (lane == 63) s_part[wv] = incl;
+    __syncthreads();
+    uint32_t woff = carry, all = carry;
+    for (uint32_t w = 0; w < GS_BIN_THREADS / 64; ++w) {
+      woff += w < wv ? s_part[w] : 0u;
+      all += s_part[w];
+    }
+    if (g < gend) s_gpre[g] = woff + incl - v;
+    carry = all;
+    __syncthreads();
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
+    total[0] = carry;
+    __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
+  }
+  if (carry > cap) return;
+  for (uint32_t k = tid; k < nt; k += GS_BIN_THREADS) {
+    const uint32_t t = t0 + k;
+    const uint2 ti = tile_info[t];
+    const uint32_t start = s_gpre[t >> 6] + ti.x;
+    s_cur[k] = hist[(size_t)c * bg.tiles + t];
+    // where the tile's pairs go: its fixed GS_TILE_SLOTS-slot row when they fit (the blend then
+    // loads keys without waiting for the range), else its segment of the pair buffer (flag bit 31)
+    s_tot[k] = ti.y <= GS_TILE_SLOTS ? t * GS_TILE_SLOTS : (start | 0x80000000u);
+    if (c == 0) ranges[t] = ti.y ? make_uint2(start, start + ti.y) : make_uint2(0u, 0u);
   }
   __syncthreads();
 #ifdef GS_PROBE_NO_WALK
   return;
 #endif
-  gs_walk_chunk(bg, rects, n, ty0, ty1, [&](uint32_t i, const ushort4& rc, uint32_t y0, uint32_t y1) {
-    const unsigned long long key = ((unsigned long long)__float_as_uint(depths[i]) << 32) | i;
-    for (uint32_t y = y0; y < y1; ++y)
-      for (uint32_t x = rc.x; x < rc.z; ++x) {
-        const uint32_t k = (y - ty0) * bg.grid_x + x;
-        const uint32_t rel = atomicAdd(s_cur + k, 1u), dst = s_tot[k];
-        if (dst & 0x80000000u)
-          pairs[(dst & 0x7FFFFFFFu) + rel] = key;
-        else
-          tile_slots[dst + rel] = key;
-      }
+  gs_walk_chunk(bg, rects, depths, n, ty0, ty1, s_q, [&](uint32_t i, uint32_t x, uint32_t y, float d) {
+    const unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | i;
+    const uint32_t k = (y - ty0) * bg.grid_x + x;
+    const uint32_t rel = atomicAdd(s_cur + k, 1u), dst = s_tot[k];
+    if (dst & 0x80000000u)
+      pairs[(dst & 0x7FFFFFFFu) + rel] = key;
+    else
+      tile_slots[dst + rel] = key;
   });
 }
 
@@ -752,29 +839,26 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = ensure(w->touched, (size_t)n * 4))) return e;
   if ((e = ensure(w->rect, (size_t)n * 8))) return e;
   if ((e = ensure(w->ranges, (size_t)tiles * 8))) return e;
-  // ~16 bands of tile rows x up to GS_BIN_CHUNKS chunks of Gaussians (~224 workgroups at 1080p)
+  // bands of as many tile rows as fit GS_BAND_TILES (1080p: one band, 4K: four) x chunks of >= GS_CHUNK_MIN
+  // Gaussians, ~256 blocks in all (at most GS_MAX_CHUNKS chunks)
   if (cam.grid_x > GS_BAND_TILES) return hipErrorInvalidValue;  // W > 131072 px
   BinGrid bgrid;
   bgrid.grid_x = cam.grid_x;
   bgrid.grid_y = cam.grid_y;
   bgrid.tiles = tiles;
-  bgrid.band_rows = std::max(1u, std::min((cam.grid_y + 15u) / 16u, GS_BAND_TILES / cam.grid_x));
+  bgrid.groups = (tiles + 63u) / 64u;
+  if (bgrid.groups > GS_MAX_GROUPS) return hipErrorInvalidValue;
+  bgrid.band_rows = std::max(1u, std::min(cam.grid_y, GS_BAND_TILES / cam.grid_x));
   bgrid.bands = std::max(1u, (cam.grid_y + bgrid.band_rows - 1) / bgrid.band_rows);
-  bgrid.chunks = std::max(1u, std::min((uint32_t)GS_BIN_CHUNKS, (n + 4095u) / 4096u));
+  bgrid.chunks = std::max(1u, std::min({(uint32_t)GS_MAX_CHUNKS, (n + GS_CHUNK_MIN - 1) / GS_CHUNK_MIN,
+                                        std::max(1u, 256u / bgrid.bands)}));
   bgrid.chunk = std::max(1u, (n + bgrid.chunks - 1) / bgrid.chunks);
   const size_t band_lds = (size_t)bgrid.band_rows * cam.grid_x * 4;
   if ((e = ensure(w->hist, (size_t)bgrid.chunks * tiles * 4))) return e;
   if ((e = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e;
-  if ((e = ensure(w->band_off, (size_t)bgrid.bands * 4))) return e;
-  if (w->band_total.bytes < (size_t)bgrid.bands * 4) {  // zero once; the count re-zeroes it every frame
-    if ((e = ensure(w->band_total, (size_t)bgrid.bands * 4))) return e;
-    if ((e = hipMemset(w->band_total.p, 0, w->band_total.bytes))) return e;
-  }
-  if (!w->ticket.p) {
-    if ((e = ensure(w->ticket, 16))) return e;
-    if ((e = hipMemset(w->ticket.p, 0, 16))) return e;
-  }
-  if (!w->total.p) {  // [0] = K, [1] = largest tile of the last scatter (see the count kernel)
+  if ((e = ensure(w->tile_info, (size_t)tiles * 8))) return e;
+  if ((e = ensure(w->group_total, (size_t)bgrid.groups * 4))) return e;
+  if (!w->total.p) {  // [0] = K (scatter), [1] = largest tile (colscan's atomicMax; count re-arms it)
     if ((e = ensure(w->total, 16))) return e;
     if ((e = hipMemset(w->total.p, 0, 16))) return e;
   }
@@ -797,7 +881,6 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     return (uint32_t)std::min<size_t>(c, 0xFFFFFFFFu);
   };
 
-  if ((e = mark(0))) return e;
   PreArgs pa;
   pa.means = g->means;
   pa.scales = g->scales;
@@ -812,27 +895,29 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   pa.touched = (uint32_t*)w->touched.p;
   pa.rects = (ushort4*)w->rect.p;
   pa.rec = (float4*)w->rec.p;
-  if (n) {
-    hipLaunchKernelGGL(gs_preprocess_kernel, dim3((n + 255) / 256), dim3(256), 0, s, cam, pa);
-    if ((e = hipGetLastError())) return e;
-  }
-  if ((e = mark(1))) return e;
-  // (n == 0: one chunk of nothing; the count still zeroes the band histograms and publishes K = 0)
-  hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), band_lds, s, bgrid,
-                     (const ushort4*)w->rect.p, n, (uint32_t*)w->hist.p, (uint32_t*)w->band_total.p,
-                     (uint32_t*)w->band_off.p, (uint32_t*)w->total.p, (uint32_t*)w->ticket.p, w->k_dev);
+  if ((e = mark(0))) return e;
+  // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
+  hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), band_lds, s, cam, pa,
+                     bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, w->k_dev);
   if ((e = hipGetLastError())) return e;
-  if ((e = hipEventRecord(w->k_event, s))) return e;
+  if ((e = mark(1))) return e;
+  hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(256), 0, s, bgrid, (uint32_t*)w->hist.p,
+                     (uint2*)w->tile_info.p, (uint32_t*)w->group_total.p, (uint32_t*)w->total.p);
+  if ((e = hipGetLastError())) return e;
   if ((e = mark(2))) return e;
 
   const uint32_t rows = cam.row_end - cam.row_begin;
+  bool first = true;
   auto enqueue_tail = [&](uint32_t cap) -> hipError_t {
-    hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), 2 * band_lds, s,
-                       bgrid, (const ushort4*)w->rect.p, (const float*)w->depths.p, n, (const uint32_t*)w->hist.p,
-                       (const uint32_t*)w->band_off.p, (uint32_t*)w->total.p, cap, (uint2*)w->ranges.p,
-                       (unsigned long long*)w->pairs.p, (unsigned long long*)w->tile_slots.p);
+    hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS),
+                       2 * band_lds + (size_t)bgrid.groups * 4, s, bgrid, (const ushort4*)w->rect.p,
+                       (const float*)w->depths.p, n, (const uint32_t*)w->hist.p, (const uint2*)w->tile_info.p,
+                       (const uint32_t*)w->group_total.p, (uint32_t*)w->total.p, w->k_dev, cap,
+                       (uint2*)w->ranges.p, (unsigned long long*)w->pairs.p, (unsigned long long*)w->tile_slots.p);
     hipError_t e2 = hipGetLastError();
     if (e2) return e2;
+    if (first && (e2 = hipEventRecord(w->k_event, s))) return e2;  // K is on the host after the scatter
+    first = false;
     if ((e2 = mark(3))) return e2;
     if ((e2 = mark(4))) return e2;
     if ((e2 = mark(5))) return e2;
@@ -853,7 +938,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = enqueue_tail(cap_now()))) return e;
   if ((e = hipEventSynchronize(w->k_event))) return e;
   const uint32_t K = w->k_host[0];
-  {  // the next frame's large-tile LDS sort capacity (k_host[1]: largest tile of an earlier frame)
+  {  // the next frame's large-tile LDS sort capacity (k_host[1]: largest tile of the previous frame)
     uint32_t want = GS_SORT_MIN;
     while (want < w->k_host[1] && want < GS_SORT_MAX) want <<= 1;
     w->lds_keys = want;

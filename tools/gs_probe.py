@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Run the C2 3DGS workload (100k Gaussians, 1920x1080) a few times (for rocprofv3 / A-B timing)."""
+"""Run the C2 3DGS workload (100k Gaussians, 1920x1080; GS_N / GS_W / GS_H override) a few times (for rocprofv3 /
+A-B timing)."""
 import os
 import sys
 import time
@@ -16,7 +17,7 @@ def main():
     variants = sys.argv[1:] or ["base"]
     iters = int(os.environ.get("GS_ITERS", "20"))
     n = int(os.environ.get("GS_N", "100000"))
-    W, H = 1920, 1080
+    W, H = int(os.environ.get("GS_W", "1920")), int(os.environ.get("GS_H", "1080"))
     g = Y.gaussians_c2(n, seed=1)
     dg = {k: torch.from_numpy(v).cuda() for k, v in g.items()}
     ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), cornell_box_scene(), 0)
