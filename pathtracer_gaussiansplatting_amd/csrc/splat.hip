@@ -50,12 +50,14 @@ struct DevBuf {
 
 struct SplatWorkspace {
   DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, tile_info,
-      group_total, tile_slots, point_keys, total, rect;
+      group_total, tile_slots, point_keys, total, rect, large, large_ctr;
   uint32_t* k_host = nullptr;  // pinned, coherent: the scan kernel stores K here
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
-  uint32_t lds_keys = 2048;  // large-tile LDS sort capacity: from the largest tile seen two frames back
+  uint32_t sort_r = 3;        // large-tile radix sort: items per work-item (from the previous frame's largest tile)
+  uint32_t sort_grid = 256;   // its workgroups (from the previous frame's large-tile count)
+  bool sort_attr = false;     // its dynamic-LDS limit raised
   hipEvent_t ev[7] = {};
   bool timed = false;
 };
@@ -66,7 +68,7 @@ void splat_workspace_destroy(SplatWorkspace* w) {
   if (!w) return;
   DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rec, &w->radii, &w->touched, &w->pairs, &w->keys_out,
                    &w->vals_out, &w->ranges, &w->hist, &w->tile_info, &w->group_total, &w->tile_slots, &w->point_keys,
-                   &w->total, &w->rect};
+                   &w->total, &w->rect, &w->large, &w->large_ctr};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
@@ -242,6 +244,18 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
 #define GS_TILE_SLOTS 256    // fixed key slots per tile (= the register-sort limit)
 #define GS_MAX_GROUPS 4096   // 64-tile groups (262144 tiles)
 
+// Inclusive wave64 prefix sum in DPP (row_shr 1/2/4/8 inside rows of 16, then row_bcast 15 / 31
+// across rows): six VALU adds instead of six ds_bpermute round trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 struct BinGrid {
   uint32_t band_rows, bands, chunks, chunk, grid_x, grid_y, tiles, groups;
 };
@@ -259,12 +273,7 @@ __device__ __forceinline__ void gs_band(const BinGrid& bg, uint32_t& ty0, uint32
 template <bool WANT_DEPTH, typename F>
 __device__ __forceinline__ void gs_expand(uint32_t lane, uint32_t eg, uint32_t exw, uint32_t eyh, float dep, F f) {
   const uint32_t a = (exw >> 16) * (eyh >> 16);
-  uint32_t incl = a;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t u = __shfl_up(incl, off);
-    if ((int)lane >= off) incl += u;
-  }
+  const uint32_t incl = wave_incl_scan(a);
   const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(incl, 63));
   const uint32_t excl = incl - a;
   for (uint32_t p = 0; p < total; p += 64) {
@@ -308,9 +317,10 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
   uint32_t base = b0 + wave * 64u;
   ushort4 pf[GS_WALK_PF];
 #pragma unroll
-  for (int k = 0; k < GS_WALK_PF; ++k) {
+  for (int k = 0; k < GS_WALK_PF; ++k) {  // (if/else: a ?: of two ushort4 lvalues selects addresses -> FLAT)
     const uint32_t i = base + k * GS_BIN_THREADS + lane;
-    pf[k] = i < b1 ? rects[i] : zero;
+    pf[k] = zero;
+    if (i < b1) pf[k] = rects[i];
   }
   uint32_t head = 0, cnt = 0;  // wave-uniform ring state
   for (;;) {
@@ -320,7 +330,8 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
       for (int k = 0; k < GS_WALK_PF - 1; ++k) pf[k] = pf[k + 1];
       {
         const uint32_t i = base + GS_WALK_PF * GS_BIN_THREADS + lane;
-        pf[GS_WALK_PF - 1] = i < b1 ? rects[i] : zero;
+        pf[GS_WALK_PF - 1] = zero;
+        if (i < b1) pf[GS_WALK_PF - 1] = rects[i];
       }
       uint32_t xw, yh;
       gs_clip(rc, ty0, ty1, xw, yh);
@@ -352,6 +363,7 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
 __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                       uint32_t* __restrict__ hist,
                                                                       uint32_t* __restrict__ total,
+                                                                      uint32_t* __restrict__ large_ctr,
                                                                       uint32_t* k_host) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
   uint32_t ty0, ty1;
@@ -361,6 +373,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam c
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);
     total[1] = 0;
+    large_ctr[0] = 0;  // large-tile list length (colscan)
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -385,12 +398,14 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam c
 
 // One 256-work-item block per 64-tile group g: wave w sums chunks [w*cpw, (w+1)*cpw) of the group's
 // 64 tiles (lane = tile: coalesced rows), then rewrites hist[c][t] as the exclusive prefix over c.
-// Outputs per tile (offset inside the group, total), per group its total, and atomicMax of the
-// largest tile into total[1].
+// Outputs per tile (offset inside the group, total), per group its total, atomicMax of the largest
+// tile into total[1], and the tiles of more than `thr` pairs appended to the large-tile list.
 __global__ __launch_bounds__(256) void gs_bin_colscan_kernel(BinGrid bg, uint32_t* __restrict__ hist,
                                                              uint2* __restrict__ tile_info,
                                                              uint32_t* __restrict__ group_total,
-                                                             uint32_t* __restrict__ total) {
+                                                             uint32_t* __restrict__ total, uint32_t thr,
+                                                             uint32_t* __restrict__ large,
+                                                             uint32_t* __restrict__ large_ctr) {
   __shared__ uint32_t s_ws[4][64];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t t = blockIdx.x * 64u + lane;
@@ -416,13 +431,16 @@ __global__ __launch_bounds__(256) void gs_bin_colscan_kernel(BinGrid bg, uint32_
     }
   if (wave != 0) return;
   const uint32_t tot = s_ws[0][lane] + s_ws[1][lane] + s_ws[2][lane] + s_ws[3][lane];
-  uint32_t incl = tot;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t u = __shfl_up(incl, off);
-    if ((int)lane >= off) incl += u;
-  }
+  const uint32_t incl = wave_incl_scan(tot);
   if (ok) tile_info[t] = make_uint2(incl - tot, tot);  // (offset inside the group, tile total)
+  const bool big = ok && tot > thr;
+  const unsigned long long bal = __ballot(big);
+  if (bal) {
+    uint32_t at = 0;
+    if (lane == 0) at = atomicAdd(large_ctr, (uint32_t)__popcll(bal));
+    at = (uint32_t)__shfl((int)at, 0);
+    if (big) large[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = t;
+  }
   uint32_t mx = tot;
   for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
   const uint32_t gsum = __shfl(incl, 63);
@@ -439,7 +457,8 @@ __global__ __launch_bounds__(256) void gs_bin_colscan_kernel(BinGrid bg, uint32_
 __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, uint32_t n,
     const uint32_t* __restrict__ hist, const uint2* __restrict__ tile_info, const uint32_t* __restrict__ group_total,
-    uint32_t* __restrict__ total, uint32_t* k_host, uint32_t cap, uint2* __restrict__ ranges,
+    uint32_t* __restrict__ total, const uint32_t* __restrict__ large_ctr, uint32_t* k_host, uint32_t cap,
+    uint2* __restrict__ ranges,
     unsigned long long* __restrict__ pairs, unsigned long long* __restrict__ tile_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];  // 2 * band_rows * grid_x + groups
   __shared__ uint4 s_q[GS_BIN_THREADS / 64 * GS_WQ];
@@ -456,12 +475,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
   for (uint32_t g0 = 0; g0 < gend; g0 += GS_BIN_THREADS) {
     const uint32_t g = g0 + tid;
     const uint32_t v = g < gend ? group_total[g] : 0u;
-    uint32_t incl = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t u = __shfl_up(incl, off);
-      if ((int)lane >= off) incl += u;
-    }
+    const uint32_t incl = wave_incl_scan(v);
     if (lane == 63) s_part[wv] = incl;
     __syncthreads();
     uint32_t woff = carry, all = carry;
@@ -475,6 +489,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
     total[0] = carry;
+    __atomic_store_n(k_host + 2, large_ctr[0], __ATOMIC_RELAXED);  // large tiles (the next sort grid)
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
   }
   if (carry > cap) return;
@@ -539,14 +554,236 @@ __device__ __forceinline__ void bitonic_flip_sort(uint32_t n, Swap swap_if) {
   }
 }
 
-// LDS arena of the blend: staged records + per-quadrant lists; a large tile's sort uses it (or more,
-// dynamic LDS) for up to lds_keys keys, above that global memory. lds_keys follows the largest tile
-// two frames back (count -> k_host[1]), between GS_SORT_MIN and GS_SORT_MAX.
-#define GS_ARENA_MIN (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)
-#define GS_SORT_MIN 2048
-#define GS_SORT_MAX 8192
+// ---- large tiles: LDS radix sort ------------------------------------------------------------------
+// Tiles of more than GS_TILE_SLOTS pairs (all non-empty tiles when the Gaussian index does not fit
+// the register sort's 24 bits) are listed by the colscan and sorted here, before the blend, by
+// 256-work-item workgroups striding over the list:
+//  load     the segment's depths (u32) and positions (u16) into LDS, padded to 256 * R (R odd, so
+//           the blocked accesses below are bank-conflict free) with depth ~0
+//  passes   stable LSD radix sort on the depth minus the tile's minimum, 4-bit digits over the bits of
+//           the depth range; work-item t owns positions [t R, t R + R): per-digit counts in packed byte
+//           registers, a (digit, work-item) scan of the 16 x 256 u16 counters in LDS, then each item
+//           goes to (its digit's scanned base) + (earlier items of that digit in the work-item)
+//  ties     equal depths are put in gaussian order (odd-even transposition inside equal-depth runs;
+//           rare: the order of a stable global sort of (tile, depth) keys over gaussian indices)
+//  publish  keys_out = tile << 32 | depth, vals_out = gaussian (the blend streams these)
+// A 16-bit-per-comparator LDS bitonic network measured ~5 MB of LDS traffic per 2.6k-pair tile
+// (LDS-bandwidth bound: ~130 us of the 1M-Gaussian frame); the radix moves ~0.2 MB.
+#define GS_SORT_THREADS 256
+#define GS_RADIX_MAXR 33  // items per work-item (odd): up to 8448 keys in LDS, global bitonic above
 
-struct GStage {  // one staged blend record (see gs_preprocess_kernel)
+__host__ __device__ constexpr size_t gs_radix_lds(uint32_t rmax) {
+  return (size_t)GS_SORT_THREADS * rmax * 12u + 16u * GS_SORT_THREADS * 2u;
+}
+
+__global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
+    const uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs,
+    const unsigned long long* __restrict__ tile_slots, const uint32_t* __restrict__ large,
+    uint32_t* __restrict__ large_ctr, unsigned long long* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+    const uint32_t* __restrict__ total, uint32_t cap, uint32_t rmax) {
+  extern __shared__ __attribute__((aligned(16))) char s_arena[];
+  // (one array per field, halves selected by offsets: an array of LDS pointers indexed at run time
+  // would turn every access into a FLAT one)
+  const uint32_t capn = GS_SORT_THREADS * rmax;
+  uint32_t* s_dep = reinterpret_cast<uint32_t*>(s_arena);           // [2][capn]
+  uint16_t* s_slot = reinterpret_cast<uint16_t*>(s_dep + 2 * capn);  // [2][capn]
+  uint16_t* s_cnt = s_slot + 2 * capn;                                // [16 digits][256 work-items]
+  __shared__ uint32_t s_red[2][GS_SORT_THREADS / 64];
+  if (*total > cap) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t count = large_ctr[0];
+  // static striding over the list (a shared work counter serialises: ~30 ns per contended atomic,
+  // 210 us for the 1M-Gaussian frame's 7k claims)
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    const uint32_t tile = large[li];
+    const uint2 range = ranges[tile];
+    const uint32_t n = range.y - range.x;
+    unsigned long long* seg = n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
+                                                 : pairs + range.x;
+    const unsigned long long tbits = (unsigned long long)tile << 32;
+    const uint32_t R = ((n + GS_SORT_THREADS - 1) / GS_SORT_THREADS) | 1u;
+    if (R > rmax) {  // beyond the LDS capacity: bitonic network in global memory (growth frames only)
+      bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
+        unsigned long long x = seg[a], y = seg[b];
+        if (y < x) { seg[a] = y; seg[b] = x; }
+      });
+      for (uint32_t k = tid; k < n; k += GS_SORT_THREADS) {
+        const unsigned long long v = seg[k];
+        keys_out[range.x + k] = tbits | (v >> 32);
+        vals_out[range.x + k] = (uint32_t)v;
+      }
+      __syncthreads();
+      continue;
+    }
+    const uint32_t np = GS_SORT_THREADS * R;
+    const uint32_t* segw = reinterpret_cast<const uint32_t*>(seg);  // (gaussian, depth) word pairs
+    uint32_t vmin = ~0u, vmax = 0u;
+    for (uint32_t k0 = tid; k0 < np; k0 += 8 * GS_SORT_THREADS) {  // 8 loads in flight per work-item
+      uint32_t d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t k = k0 + j * GS_SORT_THREADS;
+        d[j] = k < n ? segw[2 * k + 1] : ~0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t k = k0 + j * GS_SORT_THREADS;
+        if (k < n) {
+          vmin = min(vmin, d[j]);
+          vmax = max(vmax, d[j]);
+        }
+        if (k < np) {
+          s_dep[k] = d[j];
+          s_slot[k] = (uint16_t)k;
+        }
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, off));
+      vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, off));
+    }
+    if (lane == 0) {
+      s_red[0][wave] = vmin;
+      s_red[1][wave] = vmax;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < GS_SORT_THREADS / 64; ++w) {
+      vmin = min(vmin, s_red[0][w]);
+      vmax = max(vmax, s_red[1][w]);
+    }
+    // depth bits of positive floats order like the floats: sort (min(d, max) - min) over the bits of
+    // max - min only (C2's 4..12 depths: 24 bits, 6 passes); padding (~0) clamps to max and, stable
+    // and last to begin with, stays behind the real maxima
+    vmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmin);
+    vmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmax);
+    const uint32_t nbits = vmax > vmin ? 32u - (uint32_t)__builtin_clz(vmax - vmin) : 0u;
+    uint32_t cur = 0;
+    for (uint32_t sh = 0; sh < nbits; sh += 4) {
+#ifdef GS_PROBE_SORT_PASSES
+      if (sh >= 4 * GS_PROBE_SORT_PASSES) continue;
+#endif
+      const uint32_t so = cur * capn, dof = (cur ^ 1u) * capn;
+      // counts: bytes of c[0] (digits 0-7) and c[1] (digits 8-15); R <= 33 < 256
+      unsigned long long c0 = 0, c1 = 0;
+#pragma unroll 8
+      for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t d = ((min(s_dep[so + tid * R + r], vmax) - vmin) >> sh) & 15u;
+        const unsigned long long inc = 1ull << ((d & 7u) * 8u);
+        c0 += d < 8u ? inc : 0ull;
+        c1 += d < 8u ? 0ull : inc;
+      }
+#pragma unroll
+      for (uint32_t d = 0; d < 8; ++d) {
+        s_cnt[d * GS_SORT_THREADS + tid] = (uint16_t)((c0 >> (8u * d)) & 0xFFu);
+        s_cnt[(d + 8) * GS_SORT_THREADS + tid] = (uint16_t)((c1 >> (8u * d)) & 0xFFu);
+      }
+      __syncthreads();
+      // exclusive scan of the counters in (digit, work-item) order: work-item t holds entries [16t, 16t+16)
+      uint4* cw = reinterpret_cast<uint4*>(s_cnt + 16u * tid);
+      const uint4 a0 = cw[0], a1 = cw[1];
+      uint32_t v[16] = {a0.x & 0xFFFFu, a0.x >> 16, a0.y & 0xFFFFu, a0.y >> 16, a0.z & 0xFFFFu, a0.z >> 16,
+                        a0.w & 0xFFFFu, a0.w >> 16, a1.x & 0xFFFFu, a1.x >> 16, a1.y & 0xFFFFu, a1.y >> 16,
+                        a1.z & 0xFFFFu, a1.z >> 16, a1.w & 0xFFFFu, a1.w >> 16};
+      uint32_t sum = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t x = v[k];
+        v[k] = sum;
+        sum += x;
+      }
+      const uint32_t incl = wave_incl_scan(sum);
+      if (lane == 63) s_red[0][wave] = incl;
+      __syncthreads();
+      uint32_t base = incl - sum;
+      for (uint32_t w = 0; w < wave; ++w) base += s_red[0][w];
+      cw[0] = make_uint4((v[0] + base) | ((v[1] + base) << 16), (v[2] + base) | ((v[3] + base) << 16),
+                         (v[4] + base) | ((v[5] + base) << 16), (v[6] + base) | ((v[7] + base) << 16));
+      cw[1] = make_uint4((v[8] + base) | ((v[9] + base) << 16), (v[10] + base) | ((v[11] + base) << 16),
+                         (v[12] + base) | ((v[13] + base) << 16), (v[14] + base) | ((v[15] + base) << 16));
+      __syncthreads();
+      // scatter: stable inside the work-item (running byte counters), across work-items (the scan)
+      // (batches of 8: all loads of a batch issue before its stores, which the compiler may not
+      // reorder across: every array lives in the one LDS arena)
+      c0 = 0;
+      c1 = 0;
+      for (uint32_t r0 = 0; r0 < R; r0 += 8) {
+        uint32_t dv[8], sv[8], dst[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+          const uint32_t p = tid * R + min(r0 + j, R - 1);
+          dv[j] = s_dep[so + p];
+          sv[j] = s_slot[so + p];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+          const uint32_t d = ((min(dv[j], vmax) - vmin) >> sh) & 15u;
+          const uint32_t bit = (d & 7u) * 8u;
+          const unsigned long long cc = d < 8u ? c0 : c1;
+          const uint32_t local = (uint32_t)(cc >> bit) & 0xFFu;
+          const bool ok = r0 + j < R;
+          c0 += (ok && d < 8u) ? (1ull << bit) : 0ull;
+          c1 += (ok && d >= 8u) ? (1ull << bit) : 0ull;
+          dst[j] = (uint32_t)s_cnt[d * GS_SORT_THREADS + tid] + local;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+          if (r0 + j < R) {
+            s_dep[dof + dst[j]] = dv[j];
+            s_slot[dof + dst[j]] = (uint16_t)sv[j];
+          }
+      }
+      __syncthreads();
+      cur ^= 1u;
+    }
+    const uint32_t* sd = s_dep + cur * capn;
+    uint16_t* ss = s_slot + cur * capn;
+    // ties: equal depths in gaussian order
+    int tie = 0;
+    for (uint32_t k = tid; k + 1 < n; k += GS_SORT_THREADS) tie |= sd[k] == sd[k + 1];
+    if (__syncthreads_or(tie)) {
+      int changed;
+      do {
+        changed = 0;
+        for (uint32_t ph = 0; ph < 2; ++ph) {
+          for (uint32_t k = 2 * tid + ph; k + 1 < n; k += 2 * GS_SORT_THREADS)
+            if (sd[k] == sd[k + 1]) {
+              const uint16_t x = ss[k], y = ss[k + 1];
+              if (segw[2 * (uint32_t)y] < segw[2 * (uint32_t)x]) {
+                ss[k] = y;
+                ss[k + 1] = x;
+                changed = 1;
+              }
+            }
+          __syncthreads();
+        }
+      } while (__syncthreads_or(changed));
+    }
+    for (uint32_t k0 = tid; k0 < n; k0 += 8 * GS_SORT_THREADS) {  // 8 gathers in flight per work-item
+      uint32_t g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t k = k0 + j * GS_SORT_THREADS;
+        g[j] = k < n ? segw[2 * (uint32_t)ss[k]] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t k = k0 + j * GS_SORT_THREADS;
+        if (k < n) {
+          keys_out[range.x + k] = tbits | sd[k];
+          vals_out[range.x + k] = g[j];
+        }
+      }
+    }
+    __syncthreads();  // LDS reused by the next tile
+  }
+}
+
+// ---- blend ----------------------------------------------------------------------------------------
+#define GS_ARENA_MIN (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)
+#define GS_MID 512  // tiles of (256, GS_MID] pairs are sorted inside the blend (rank counting)
+
+struct GStage {  // one staged blend record (see gs_preprocess_one)
   float4 a, b, c;
 };
 
@@ -555,11 +792,12 @@ struct GStage {  // one staged blend record (see gs_preprocess_kernel)
 // dispatcher's dynamic balancing, 103 vs 72 us at C2; a tile-pair workgroup shading two pixels per
 // lane in packed f32 measured 133 vs 104 us per frame: the per-pixel done / valid bookkeeping of the
 // pair and the strip lists cost more than the packing saved).
-//  sort     the tile's pairs by (depth, gaussian): tiles of <= 256 pairs in registers (one key per
-//           work-item; while the network runs, the blend records of the unsorted keys are already
-//           in flight, the key carries its staging slot in its low 8 bits); larger tiles in LDS
-//           (global memory above lds_keys) with records staged in batches of 256.
-//  publish  the sorted keys (tile << 32 | depth) / values (gaussian).
+//  sort     tiles of <= 256 pairs: in registers (one key per work-item; while the network runs, the
+//           blend records of the unsorted keys are already in flight, the key carries its staging
+//           slot in its low 8 bits), then publish the sorted keys (tile << 32 | depth) / values
+//           (gaussian). Larger tiles were sorted and published by gs_sort_large_kernel: their values
+//           are streamed in batches of 256, the records of batch b + 1 (and the values of b + 2) in
+//           flight while batch b blends.
 //  blend    wave w shades the 8x8 quadrant q = w of the tile (x half w & 1, y half w >> 1), one pixel
 //           per lane. Each staged Gaussian's alpha box is tested against the four quadrants; a ballot
 //           + LDS offsets compact that into four ordered per-quadrant lists, so a wave iterates only
@@ -570,6 +808,7 @@ struct GStage {  // one staged blend record (see gs_preprocess_kernel)
 template <bool OVER>
 __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, const uint2* __restrict__ ranges,
                                                                  unsigned long long* __restrict__ pairs,
+                                                                 uint32_t sorted_above,
                                                                  unsigned long long* __restrict__ keys_out,
                                                                  uint32_t* __restrict__ vals_out,
                                                                  const float4* __restrict__ rec, float bg_r,
@@ -579,17 +818,13 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
                                                                  const unsigned long long* __restrict__ tile_slots,
                                                                  const float* __restrict__ depth_lim,
                                                                  const float4* __restrict__ under,
-                                                                 float4* __restrict__ out, uint32_t lds_keys) {
+                                                                 float4* __restrict__ out) {
   // staged records of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads the
-  // per-quadrant lists to a multiple of 4
-  // One LDS arena: the staged records and the per-quadrant lists (byte offsets into the records).
-  // The sorts' key arrays alias it (the register network's 64 / 128 exchanges: 256 keys; a large
-  // tile: <= lds_keys keys), which is safe because records and lists are written only after
-  // the sort, behind a barrier; the sorted keys / values are read back from keys_out / vals_out.
-  extern __shared__ __attribute__((aligned(16))) char s_arena[];  // max(GS_ARENA_MIN, 8 * lds_keys) bytes
+  // per-quadrant lists to a multiple of 4.
+  __shared__ __attribute__((aligned(16))) char s_arena[GS_ARENA_MIN];
   GStage* s_stage = reinterpret_cast<GStage*>(s_arena);
   uint32_t(*s_list)[GS_BLOCK + 4] = reinterpret_cast<uint32_t(*)[GS_BLOCK + 4]>(s_arena + sizeof(GStage) * (GS_BLOCK + 1));
-  unsigned long long* s_key = reinterpret_cast<unsigned long long*>(s_arena);
+  __shared__ unsigned long long s_key[GS_MID];  // register-sort exchanges; a mid tile's sorted keys
   __shared__ uint8_t s_mask[GS_BLOCK];
   __shared__ uint32_t s_qcnt[4][4];  // [wave][quadrant]
   if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
@@ -617,16 +852,14 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
   const uint32_t n = range.y - range.x;
 #endif
   const bool small = slot_keys && n <= GS_BLOCK;
-  const bool in_lds = n <= lds_keys;
-  // where the scatter put this tile's keys: its slot row (<= GS_TILE_SLOTS) or its pair segment
-  unsigned long long* seg = n <= GS_TILE_SLOTS
-                                ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
-                                : pairs + range.x;
+  const bool mid = !small && n <= sorted_above;  // not sorted by gs_sort_large_kernel: sorted here
+  const bool mid_lds = mid && n <= GS_MID;
   const unsigned long long tbits = (unsigned long long)tile << 32;
   uint32_t my_slot = 0;  // small tiles: staging slot of sorted element tid
-  float4 ra, rb, rc;
+  float4 ra, rb, rc;     // records in flight: the unsorted keys' (small) / batch b + 1's (large)
+  uint32_t g_next = 0;   // large tiles: gaussian of batch b + 2
   unsigned long long key = ~0ull;
-  if (small && tid < n) {  // records are in flight while the network runs
+  if (small && tid < n) {
     const unsigned long long k_cur = k_slot;
     const uint32_t g = (uint32_t)k_cur;
 #ifdef GS_PROBE_NO_REC
@@ -663,7 +896,6 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
         const bool swap = (other < key) == (((tid & j) == 0) == ((tid & k) == 0));
         key = swap ? other : key;
       }
-    if (npad >= 128) __syncthreads();  // the last exchange reads are done before records overwrite them
     if (tid < n) {
       s_stage[tid].a = ra;
       s_stage[tid].b = rb;
@@ -676,27 +908,53 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
       my_slot = (uint32_t)key & 0xFFu;
     }
   } else {
-    if (in_lds) {
-      for (uint32_t k = tid; k < n; k += GS_BLOCK) s_key[k] = seg[k];
-      __syncthreads();
-#ifndef GS_PROBE_NO_BIGSORT
-      bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
-        unsigned long long x = s_key[a], y = s_key[b];
-        if (y < x) { s_key[a] = y; s_key[b] = x; }
-      });
-#endif
-    } else {
-      bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
-        unsigned long long x = seg[a], y = seg[b];
-        if (y < x) { seg[a] = y; seg[b] = x; }
-      });
+    if (mid) {
+      unsigned long long* seg = n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
+                                                   : pairs + range.x;
+      if (mid_lds) {
+        // rank by counting (keys are unique: the gaussian is in the low word): each work-item ranks
+        // its two keys against all n in LDS (uniform reads), then writes them to their ranks
+        const unsigned long long k0 = tid < n ? seg[tid] : ~0ull;
+        const unsigned long long k1 = tid + GS_BLOCK < n ? seg[tid + GS_BLOCK] : ~0ull;
+        s_key[tid] = k0;
+        s_key[tid + GS_BLOCK] = k1;
+        __syncthreads();
+        uint32_t r0 = 0, r1 = 0;
+        for (uint32_t j = 0; j < n; j += 2) {
+          const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(s_key + j);
+          r0 += (x.x < k0) + (x.y < k0);
+          r1 += (x.x < k1) + (x.y < k1);
+        }
+        __syncthreads();
+        if (tid < n) s_key[r0] = k0;
+        if (tid + GS_BLOCK < n) s_key[r1] = k1;
+        __syncthreads();
+        for (uint32_t k = tid; k < n; k += GS_BLOCK) {
+          const unsigned long long v = s_key[k];
+          keys_out[range.x + k] = tbits | (v >> 32);
+          vals_out[range.x + k] = (uint32_t)v;
+        }
+      } else {  // beyond GS_MID without the sort kernel (a frame whose tiles outgrew the previous one's)
+        bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
+          unsigned long long x = seg[a], y = seg[b];
+          if (y < x) { seg[a] = y; seg[b] = x; }
+        });
+        for (uint32_t k = tid; k < n; k += GS_BLOCK) {
+          const unsigned long long v = seg[k];
+          keys_out[range.x + k] = tbits | (v >> 32);
+          vals_out[range.x + k] = (uint32_t)v;
+        }
+        __syncthreads();
+      }
     }
-    for (uint32_t k = tid; k < n; k += GS_BLOCK) {
-      unsigned long long v = in_lds ? s_key[k] : seg[k];
-      keys_out[range.x + k] = tbits | (v >> 32);
-      vals_out[range.x + k] = (uint32_t)v;
+    // sorted values (LDS for mid tiles, else vals_out): batch 0's records and batch 1's values in flight
+    if (tid < n) {
+      const uint32_t g = mid_lds ? (uint32_t)s_key[tid] : vals_out[range.x + tid];
+      ra = rec[3 * g];
+      rb = rec[3 * g + 1];
+      rc = rec[3 * g + 2];
     }
-    __syncthreads();  // sorted keys consumed: the arena becomes records / lists; batches read vals_out
+    if (tid + GS_BLOCK < n) g_next = mid_lds ? (uint32_t)s_key[tid + GS_BLOCK] : vals_out[range.x + tid + GS_BLOCK];
   }
   if (tid == 0) {  // the null record (alpha 0) that pads the per-quadrant lists
     s_stage[GS_BLOCK].a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -716,7 +974,8 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
   const char* stage = reinterpret_cast<const char*>(s_stage);
   int todo = (int)n;
   for (uint32_t base = 0; todo > 0; base += GS_BLOCK, todo -= GS_BLOCK) {
-    // (small tiles: the barrier also publishes the records and masks staged after the sort)
+    // (small tiles: the barrier also publishes the records and masks staged after the sort; large
+    // tiles: the previous batch's lists have been consumed)
     if (__syncthreads_count(done) == GS_BLOCK) break;
     const uint32_t idx = base + tid;
     uint32_t m = 0, slot = tid;
@@ -725,13 +984,21 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
         slot = my_slot;
         m = s_mask[slot];
       }
-    } else if (idx < n) {
-      const uint32_t g = vals_out[range.x + idx];
-      const float4 ga = rec[3 * g], gb = rec[3 * g + 1], gc = rec[3 * g + 2];
-      s_stage[tid].a = ga;
-      s_stage[tid].b = gb;
-      s_stage[tid].c = gc;
-      m = quad_mask(ga, gc);
+    } else {
+      if (idx < n) {
+        s_stage[tid].a = ra;
+        s_stage[tid].b = rb;
+        s_stage[tid].c = rc;
+        m = quad_mask(ra, rc);
+      }
+      // next batch: its records (values loaded a batch ago) and the values of the one after
+      if (idx + GS_BLOCK < n) {
+        const uint32_t g = g_next;
+        ra = rec[3 * g];
+        rb = rec[3 * g + 1];
+        rc = rec[3 * g + 2];
+      }
+      if (idx + 2 * GS_BLOCK < n) g_next = vals_out[range.x + idx + 2 * GS_BLOCK];
     }
     uint32_t rank[4];
 #pragma unroll
@@ -858,6 +1125,11 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e;
   if ((e = ensure(w->tile_info, (size_t)tiles * 8))) return e;
   if ((e = ensure(w->group_total, (size_t)bgrid.groups * 4))) return e;
+  if ((e = ensure(w->large, (size_t)tiles * 4))) return e;
+  if (!w->large_ctr.p) {
+    if ((e = ensure(w->large_ctr, 16))) return e;
+    if ((e = hipMemset(w->large_ctr.p, 0, 16))) return e;
+  }
   if (!w->total.p) {  // [0] = K (scatter), [1] = largest tile (colscan's atomicMax; count re-arms it)
     if ((e = ensure(w->total, 16))) return e;
     if ((e = hipMemset(w->total.p, 0, 16))) return e;
@@ -881,6 +1153,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     return (uint32_t)std::min<size_t>(c, 0xFFFFFFFFu);
   };
 
+  const uint32_t slot_keys = n < (1u << 24) ? 1u : 0u;  // the register sort packs the gaussian in 24 bits
   PreArgs pa;
   pa.means = g->means;
   pa.scales = g->scales;
@@ -898,11 +1171,12 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = mark(0))) return e;
   // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
   hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), band_lds, s, cam, pa,
-                     bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, w->k_dev);
+                     bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev);
   if ((e = hipGetLastError())) return e;
   if ((e = mark(1))) return e;
   hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(256), 0, s, bgrid, (uint32_t*)w->hist.p,
-                     (uint2*)w->tile_info.p, (uint32_t*)w->group_total.p, (uint32_t*)w->total.p);
+                     (uint2*)w->tile_info.p, (uint32_t*)w->group_total.p, (uint32_t*)w->total.p, (uint32_t)GS_MID,
+                     (uint32_t*)w->large.p, (uint32_t*)w->large_ctr.p);
   if ((e = hipGetLastError())) return e;
   if ((e = mark(2))) return e;
 
@@ -912,25 +1186,40 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS),
                        2 * band_lds + (size_t)bgrid.groups * 4, s, bgrid, (const ushort4*)w->rect.p,
                        (const float*)w->depths.p, n, (const uint32_t*)w->hist.p, (const uint2*)w->tile_info.p,
-                       (const uint32_t*)w->group_total.p, (uint32_t*)w->total.p, w->k_dev, cap,
+                       (const uint32_t*)w->group_total.p, (uint32_t*)w->total.p, (const uint32_t*)w->large_ctr.p, w->k_dev, cap,
                        (uint2*)w->ranges.p, (unsigned long long*)w->pairs.p, (unsigned long long*)w->tile_slots.p);
     hipError_t e2 = hipGetLastError();
     if (e2) return e2;
     if (first && (e2 = hipEventRecord(w->k_event, s))) return e2;  // K is on the host after the scatter
     first = false;
     if ((e2 = mark(3))) return e2;
+    // tiles above GS_MID pairs: sorted by gs_sort_large_kernel when the previous frame had any (else
+    // the blend sorts the rare one itself)
+    const bool sort_large = w->k_host[1] > GS_MID;
+    if (sort_large) {
+      if (!w->sort_attr) {
+        if ((e2 = hipFuncSetAttribute((const void*)gs_sort_large_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)gs_radix_lds(GS_RADIX_MAXR))))
+          return e2;
+        w->sort_attr = true;
+      }
+      hipLaunchKernelGGL(gs_sort_large_kernel, dim3(w->sort_grid), dim3(GS_SORT_THREADS), gs_radix_lds(w->sort_r), s,
+                       (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
+                       (const unsigned long long*)w->tile_slots.p, (const uint32_t*)w->large.p,
+                       (uint32_t*)w->large_ctr.p, (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p,
+                       (const uint32_t*)w->total.p, cap, w->sort_r);
+      if ((e2 = hipGetLastError())) return e2;
+    }
     if ((e2 = mark(4))) return e2;
     if ((e2 = mark(5))) return e2;
     if (rows > 0) {
       auto k = depth ? gs_sort_blend_kernel<true> : gs_sort_blend_kernel<false>;
       const dim3 grid(cam.grid_x, rows);
-      const size_t lds = std::max((size_t)GS_ARENA_MIN, (size_t)w->lds_keys * 8u);
-      hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), lds, s, cam, (const uint2*)w->ranges.p,
-                         (unsigned long long*)w->pairs.p, (unsigned long long*)w->keys_out.p,
-                         (uint32_t*)w->vals_out.p, (const float4*)w->rec.p, bg[0], bg[1], bg[2],
-                         (const uint32_t*)w->total.p, cap, n < (1u << 24) ? 1u : 0u,
-                         (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out,
-                         w->lds_keys);
+      hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p,
+                         (unsigned long long*)w->pairs.p, sort_large ? (uint32_t)GS_MID : 0xFFFFFFFFu,
+                         (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p, (const float4*)w->rec.p,
+                         bg[0], bg[1], bg[2], (const uint32_t*)w->total.p, cap, slot_keys,
+                         (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out);
       if ((e2 = hipGetLastError())) return e2;
     }
     return mark(6);
@@ -938,10 +1227,11 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = enqueue_tail(cap_now()))) return e;
   if ((e = hipEventSynchronize(w->k_event))) return e;
   const uint32_t K = w->k_host[0];
-  {  // the next frame's large-tile LDS sort capacity (k_host[1]: largest tile of the previous frame)
-    uint32_t want = GS_SORT_MIN;
-    while (want < w->k_host[1] && want < GS_SORT_MAX) want <<= 1;
-    w->lds_keys = want;
+  {  // the next frame's large-tile sort: LDS capacity from the largest tile of the previous frame
+     // (k_host[1]; +1/8 headroom), persistent workgroups from this frame's large-tile count (k_host[2])
+    const uint32_t big = w->k_host[1] + w->k_host[1] / 8u;
+    w->sort_r = std::min((uint32_t)GS_RADIX_MAXR, ((big + GS_SORT_THREADS - 1) / GS_SORT_THREADS) | 1u);
+    w->sort_grid = std::max(64u, std::min(4096u, w->k_host[2] + w->k_host[2] / 4u));
   }
   if (K > cap_now()) {  // did not fit: grow (hipFree/hipMalloc order after the no-op kernels) and re-run
     if ((e = ensure(w->pairs, (size_t)K * 8))) return e;

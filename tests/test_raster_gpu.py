@@ -65,6 +65,32 @@ def test_gaussians_parity(renderer, oracle_lib, n, W, H):
     print(f"gaussians n={n} K={ref['K']} rel L2 {err:.2e} differing px {int(np.count_nonzero(np.any(img != ref['image'], -1)))}")
 
 
+@pytest.mark.parametrize("n,W,H", [(20000, 320, 180),      # tiles of 256-1000 pairs: in-blend and radix sorts
+                                   (300000, 1920, 1080),   # C2 layout at 3x the density: thousands of large tiles
+                                   (3000, 48, 40)])        # ~3k pairs per tile
+def test_gaussians_large_tile_sorts(renderer, oracle_lib, n, W, H):
+    """Tiles above 256 pairs: the first frame after a smaller one sorts them inside the blend (rank
+    counting up to 512, bitonic above), later frames in gs_sort_large_kernel (LDS radix sort) - both
+    must give the oracle's sorted keys / values bit for bit, including equal-depth ties."""
+    g = Y.gaussians_c2(n, seed=5)
+    g["means"][1::97] = g["means"][0::97][: len(g["means"][1::97])]  # duplicated means: equal depths
+    ubo = _gauss_ubo(W, H)
+    dg = {k: _dev(v) for k, v in g.items()}
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H)
+    tiny = {k: _dev(v) for k, v in Y.gaussians_c2(10, seed=1).items()}
+    renderer.splat_gaussians(tiny, ubo, W, H, torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"))
+    for frame in range(2):  # frame 0: after a small frame (in-blend sorts); frame 1: the radix kernel
+        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        st = renderer.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
+        torch.cuda.synchronize()
+        b = renderer.splat_buffers()
+        assert st.num_rendered == ref["K"]
+        np.testing.assert_array_equal(_read(renderer, b.sorted_keys, ref["K"], np.uint64), ref["keys"])
+        np.testing.assert_array_equal(_read(renderer, b.sorted_values, ref["K"], np.uint32), ref["vals"])
+        err = U.rel_l2(out.cpu().numpy(), ref["image"])
+        assert err < 1e-4, (frame, err)
+
+
 def test_gaussians_tile_row_shards_compose(renderer):
     """§8e screen-tile shard: rendering tile rows [0,a) and [a,gy) separately == the full frame."""
     n, W, H = 5000, 200, 120
