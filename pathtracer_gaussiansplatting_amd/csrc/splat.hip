@@ -50,7 +50,7 @@ struct DevBuf {
 
 struct SplatWorkspace {
   DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, tile_info,
-      group_total, tile_slots, point_keys, total, rect, large, large_ctr;
+      group_total, tile_slots, point_keys, total, rect, large, large_ctr, sort_scratch;
   uint32_t* k_host = nullptr;  // pinned, coherent: the scan kernel stores K here
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
@@ -68,7 +68,7 @@ void splat_workspace_destroy(SplatWorkspace* w) {
   if (!w) return;
   DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rec, &w->radii, &w->touched, &w->pairs, &w->keys_out,
                    &w->vals_out, &w->ranges, &w->hist, &w->tile_info, &w->group_total, &w->tile_slots, &w->point_keys,
-                   &w->total, &w->rect, &w->large, &w->large_ctr};
+                   &w->total, &w->rect, &w->large, &w->large_ctr, &w->sort_scratch};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
@@ -358,8 +358,7 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
   }
 }
 
-// preprocess + count. Block (0, 0) also hands the previous frame's largest tile (total[1], colscan's
-// atomicMax) to the host (the blend's LDS sort capacity) and re-arms it.
+// preprocess + count. Block (0, 0) also re-arms the frame's counters.
 __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                       uint32_t* __restrict__ hist,
                                                                       uint32_t* __restrict__ total,
@@ -371,8 +370,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam c
   const uint32_t nt = (ty1 - ty0) * bg.grid_x;
   for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) s_hist[k] = 0;
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);
-    total[1] = 0;
+    total[1] = 0;  // largest tile (colscan's atomicMax; the scatter hands it to the host)
     large_ctr[0] = 0;  // large-tile list length (colscan)
   }
   __syncthreads();
@@ -451,7 +449,7 @@ __global__ __launch_bounds__(256) void gs_bin_colscan_kernel(BinGrid bg, uint32_
 }
 
 // K = the sum of the group totals (every block scans them all); block (0, 0) publishes it to total[0]
-// (the blend's check) and to pinned host memory. Pairs are written only when K fits the pair buffer
+// (the blend's check) and, with the largest tile and the large-tile count, to pinned host memory. Pairs are written only when K fits the pair buffer
 // (the host sizes it from the previous K and re-runs scatter + blend after growing it when it did
 // not: see splat_gaussians).
 __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
@@ -489,6 +487,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
     total[0] = carry;
+    __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);      // largest tile (the next sort's LDS size)
     __atomic_store_n(k_host + 2, large_ctr[0], __ATOMIC_RELAXED);  // large tiles (the next sort grid)
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
   }
@@ -554,43 +553,218 @@ __device__ __forceinline__ void bitonic_flip_sort(uint32_t n, Swap swap_if) {
   }
 }
 
-// ---- large tiles: LDS radix sort ------------------------------------------------------------------
-// Tiles of more than GS_TILE_SLOTS pairs (all non-empty tiles when the Gaussian index does not fit
-// the register sort's 24 bits) are listed by the colscan and sorted here, before the blend, by
+// ---- large tiles: radix sort ----------------------------------------------------------------------
+// Tiles of more than GS_MID pairs are listed by the colscan and sorted here, before the blend, by
 // 256-work-item workgroups striding over the list:
-//  load     the segment's depths (u32) and positions (u16) into LDS, padded to 256 * R (R odd, so
-//           the blocked accesses below are bank-conflict free) with depth ~0
-//  passes   stable LSD radix sort on the depth minus the tile's minimum, 4-bit digits over the bits of
-//           the depth range; work-item t owns positions [t R, t R + R): per-digit counts in packed byte
+//  load     the segment's depths (u32) and positions (u16) into LDS (tiles of up to 256 * rmax
+//           pairs; rmax follows the previous frame's largest tile) or, above that, into a global
+//           scratch at the tile's pair offset (10M Gaussians at 4K: ~28k-pair tiles, L2-resident)
+//  passes   stable LSD radix sort on the depth minus the tile's minimum, 4-bit digits over the bits
+//           of the depth range (C2's 4..12 depths: 24 bits, 6 passes); work-item t owns positions
+//           [t R, t R + R) (R odd: bank-conflict free in LDS): per-digit counts in packed byte
 //           registers, a (digit, work-item) scan of the 16 x 256 u16 counters in LDS, then each item
 //           goes to (its digit's scanned base) + (earlier items of that digit in the work-item)
 //  ties     equal depths are put in gaussian order (odd-even transposition inside equal-depth runs;
 //           rare: the order of a stable global sort of (tile, depth) keys over gaussian indices)
 //  publish  keys_out = tile << 32 | depth, vals_out = gaussian (the blend streams these)
-// A 16-bit-per-comparator LDS bitonic network measured ~5 MB of LDS traffic per 2.6k-pair tile
+// A 16-byte-per-comparator LDS bitonic network measured ~5 MB of LDS traffic per 2.6k-pair tile
 // (LDS-bandwidth bound: ~130 us of the 1M-Gaussian frame); the radix moves ~0.2 MB.
 #define GS_SORT_THREADS 256
-#define GS_RADIX_MAXR 33  // items per work-item (odd): up to 8448 keys in LDS, global bitonic above
+#define GS_RADIX_MAXR 33      // items per work-item (odd) in LDS: up to 8448 keys
+#define GS_RADIX_MAXN 65535u  // u16 positions: global bitonic above (never met by the configs)
 
 __host__ __device__ constexpr size_t gs_radix_lds(uint32_t rmax) {
   return (size_t)GS_SORT_THREADS * rmax * 12u + 16u * GS_SORT_THREADS * 2u;
 }
 
+// Sort positions [0, n) of (dep[0], slot[0]) (dep[1] / slot[1]: the other half of the ping-pong) by
+// depth; returns the half that holds the result. DEP / SLOT are LDS or global arrays (inlined per
+// call site, so the address spaces are known); s_cnt and s_red are LDS.
+__device__ __forceinline__ uint32_t gs_radix_tile(uint32_t* dep0, uint32_t* dep1, uint16_t* slot0, uint16_t* slot1,
+                                                  uint16_t* s_cnt, uint32_t (*s_red)[GS_SORT_THREADS / 64],
+                                                  const uint32_t* segw, uint32_t n, uint32_t R) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t vmin = ~0u, vmax = 0u;
+  for (uint32_t k0 = tid; k0 < n; k0 += 8 * GS_SORT_THREADS) {  // 8 loads in flight per work-item
+    uint32_t d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t k = k0 + j * GS_SORT_THREADS;
+      d[j] = k < n ? segw[2 * k + 1] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t k = k0 + j * GS_SORT_THREADS;
+      if (k < n) {
+        vmin = min(vmin, d[j]);
+        vmax = max(vmax, d[j]);
+        dep0[k] = d[j];
+        slot0[k] = (uint16_t)k;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, off));
+    vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, off));
+  }
+  if (lane == 0) {
+    s_red[0][wave] = vmin;
+    s_red[1][wave] = vmax;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < GS_SORT_THREADS / 64; ++w) {
+    vmin = min(vmin, s_red[0][w]);
+    vmax = max(vmax, s_red[1][w]);
+  }
+  // depth bits of positive floats order like the floats: sort (d - min) over the bits of max - min
+  vmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmin);
+  vmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmax);
+  const uint32_t nbits = vmax > vmin ? 32u - (uint32_t)__builtin_clz(vmax - vmin) : 0u;
+  const uint32_t p0 = tid * R, p1 = min(n, p0 + R);  // this work-item's positions
+  uint32_t cur = 0;
+  for (uint32_t sh = 0; sh < nbits; sh += 4) {
+#ifdef GS_PROBE_SORT_PASSES
+    if (sh >= 4 * GS_PROBE_SORT_PASSES) continue;
+#endif
+    const uint32_t* sd = cur ? dep1 : dep0;
+    const uint16_t* ss = cur ? slot1 : slot0;
+    uint32_t* dd = cur ? dep0 : dep1;
+    uint16_t* ds = cur ? slot0 : slot1;
+    // counts: bytes of c0 (digits 0-7) and c1 (digits 8-15); R < 256
+    unsigned long long c0 = 0, c1 = 0;
+#pragma unroll 8
+    for (uint32_t p = p0; p < p1; ++p) {
+      const uint32_t d = ((sd[p] - vmin) >> sh) & 15u;
+      const unsigned long long inc = 1ull << ((d & 7u) * 8u);
+      c0 += d < 8u ? inc : 0ull;
+      c1 += d < 8u ? 0ull : inc;
+    }
+#pragma unroll
+    for (uint32_t d = 0; d < 8; ++d) {
+      s_cnt[d * GS_SORT_THREADS + tid] = (uint16_t)((c0 >> (8u * d)) & 0xFFu);
+      s_cnt[(d + 8) * GS_SORT_THREADS + tid] = (uint16_t)((c1 >> (8u * d)) & 0xFFu);
+    }
+    __syncthreads();
+    // exclusive scan of the counters in (digit, work-item) order: work-item t holds entries [16t, 16t+16)
+    uint4* cw = reinterpret_cast<uint4*>(s_cnt + 16u * tid);
+    const uint4 a0 = cw[0], a1 = cw[1];
+    uint32_t v[16] = {a0.x & 0xFFFFu, a0.x >> 16, a0.y & 0xFFFFu, a0.y >> 16, a0.z & 0xFFFFu, a0.z >> 16,
+                      a0.w & 0xFFFFu, a0.w >> 16, a1.x & 0xFFFFu, a1.x >> 16, a1.y & 0xFFFFu, a1.y >> 16,
+                      a1.z & 0xFFFFu, a1.z >> 16, a1.w & 0xFFFFu, a1.w >> 16};
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t x = v[k];
+      v[k] = sum;
+      sum += x;
+    }
+    const uint32_t incl = wave_incl_scan(sum);
+    if (lane == 63) s_red[0][wave] = incl;
+    __syncthreads();
+    uint32_t base = incl - sum;
+    for (uint32_t w = 0; w < wave; ++w) base += s_red[0][w];
+    cw[0] = make_uint4((v[0] + base) | ((v[1] + base) << 16), (v[2] + base) | ((v[3] + base) << 16),
+                       (v[4] + base) | ((v[5] + base) << 16), (v[6] + base) | ((v[7] + base) << 16));
+    cw[1] = make_uint4((v[8] + base) | ((v[9] + base) << 16), (v[10] + base) | ((v[11] + base) << 16),
+                       (v[12] + base) | ((v[13] + base) << 16), (v[14] + base) | ((v[15] + base) << 16));
+    __syncthreads();
+    // scatter, stable inside the work-item (running byte counters) and across work-items (the scan);
+    // batches of 8: a batch's loads issue before its stores (which the compiler may not reorder
+    // across: every array can alias)
+    c0 = 0;
+    c1 = 0;
+    for (uint32_t q0 = p0; q0 < p1; q0 += 8) {
+      uint32_t dv[8], sv[8], dst[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t p = min(q0 + j, p1 - 1);
+        dv[j] = sd[p];
+        sv[j] = ss[p];
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t d = ((dv[j] - vmin) >> sh) & 15u;
+        const uint32_t bit = (d & 7u) * 8u;
+        const unsigned long long cc = d < 8u ? c0 : c1;
+        const uint32_t local = (uint32_t)(cc >> bit) & 0xFFu;
+        const bool ok = q0 + j < p1;
+        c0 += (ok && d < 8u) ? (1ull << bit) : 0ull;
+        c1 += (ok && d >= 8u) ? (1ull << bit) : 0ull;
+        dst[j] = (uint32_t)s_cnt[d * GS_SORT_THREADS + tid] + local;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j)
+        if (q0 + j < p1) {
+          dd[dst[j]] = dv[j];
+          ds[dst[j]] = (uint16_t)sv[j];
+        }
+    }
+    __syncthreads();
+    cur ^= 1u;
+  }
+  return cur;
+}
+
+// ties (equal depths in gaussian order) and publish of one sorted tile
+__device__ __forceinline__ void gs_radix_publish(const uint32_t* sd, uint16_t* ss, const uint32_t* segw, uint32_t n,
+                                                 unsigned long long tbits, unsigned long long* keys_out,
+                                                 uint32_t* vals_out) {
+  const uint32_t tid = threadIdx.x;
+  int tie = 0;
+  for (uint32_t k = tid; k + 1 < n; k += GS_SORT_THREADS) tie |= sd[k] == sd[k + 1];
+  if (__syncthreads_or(tie)) {
+    int changed;
+    do {
+      changed = 0;
+      for (uint32_t ph = 0; ph < 2; ++ph) {
+        for (uint32_t k = 2 * tid + ph; k + 1 < n; k += 2 * GS_SORT_THREADS)
+          if (sd[k] == sd[k + 1]) {
+            const uint16_t x = ss[k], y = ss[k + 1];
+            if (segw[2 * (uint32_t)y] < segw[2 * (uint32_t)x]) {
+              ss[k] = y;
+              ss[k + 1] = x;
+              changed = 1;
+            }
+          }
+        __syncthreads();
+      }
+    } while (__syncthreads_or(changed));
+  }
+  for (uint32_t k0 = tid; k0 < n; k0 += 8 * GS_SORT_THREADS) {  // 8 gathers in flight per work-item
+    uint32_t g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t k = k0 + j * GS_SORT_THREADS;
+      g[j] = k < n ? segw[2 * (uint32_t)ss[k]] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t k = k0 + j * GS_SORT_THREADS;
+      if (k < n) {
+        keys_out[k] = tbits | sd[k];
+        vals_out[k] = g[j];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
     const uint2* __restrict__ ranges, unsigned long long* __restrict__ pairs,
     const unsigned long long* __restrict__ tile_slots, const uint32_t* __restrict__ large,
-    uint32_t* __restrict__ large_ctr, unsigned long long* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    const uint32_t* __restrict__ total, uint32_t cap, uint32_t rmax) {
+    const uint32_t* __restrict__ large_ctr, unsigned long long* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+    const uint32_t* __restrict__ total, uint32_t cap, uint32_t rmax, uint32_t* __restrict__ g_dep,
+    uint16_t* __restrict__ g_slot, uint32_t g_cap) {
+  // LDS: one array per field, halves at offsets (an array of LDS pointers indexed at run time would
+  // turn every access into a FLAT one)
   extern __shared__ __attribute__((aligned(16))) char s_arena[];
-  // (one array per field, halves selected by offsets: an array of LDS pointers indexed at run time
-  // would turn every access into a FLAT one)
   const uint32_t capn = GS_SORT_THREADS * rmax;
   uint32_t* s_dep = reinterpret_cast<uint32_t*>(s_arena);           // [2][capn]
   uint16_t* s_slot = reinterpret_cast<uint16_t*>(s_dep + 2 * capn);  // [2][capn]
   uint16_t* s_cnt = s_slot + 2 * capn;                                // [16 digits][256 work-items]
   __shared__ uint32_t s_red[2][GS_SORT_THREADS / 64];
   if (*total > cap) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x;
   const uint32_t count = large_ctr[0];
   // static striding over the list (a shared work counter serialises: ~30 ns per contended atomic,
   // 210 us for the 1M-Gaussian frame's 7k claims)
@@ -600,9 +774,20 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
     const uint32_t n = range.y - range.x;
     unsigned long long* seg = n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
                                                  : pairs + range.x;
+    const uint32_t* segw = reinterpret_cast<const uint32_t*>(seg);  // (gaussian, depth) word pairs
     const unsigned long long tbits = (unsigned long long)tile << 32;
     const uint32_t R = ((n + GS_SORT_THREADS - 1) / GS_SORT_THREADS) | 1u;
-    if (R > rmax) {  // beyond the LDS capacity: bitonic network in global memory (growth frames only)
+    if (R <= rmax) {
+      const uint32_t h = gs_radix_tile(s_dep, s_dep + capn, s_slot, s_slot + capn, s_cnt, s_red, segw, n, R);
+      gs_radix_publish(s_dep + h * capn, s_slot + h * capn, segw, n, tbits, keys_out + range.x, vals_out + range.x);
+    } else if (g_dep && n <= GS_RADIX_MAXN && range.y <= g_cap) {
+      // global scratch at the tile's pair offset: [2][g_cap] depths, [2][g_cap] positions
+      uint32_t* d0 = g_dep + range.x;
+      uint16_t* s0 = g_slot + range.x;
+      const uint32_t h = gs_radix_tile(d0, d0 + g_cap, s0, s0 + g_cap, s_cnt, s_red, segw, n, R);
+      gs_radix_publish(h ? d0 + g_cap : d0, h ? s0 + g_cap : s0, segw, n, tbits, keys_out + range.x,
+                       vals_out + range.x);
+    } else {  // bitonic network in global memory (a frame whose tiles outgrew the scratch)
       bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
         unsigned long long x = seg[a], y = seg[b];
         if (y < x) { seg[a] = y; seg[b] = x; }
@@ -611,168 +796,6 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
         const unsigned long long v = seg[k];
         keys_out[range.x + k] = tbits | (v >> 32);
         vals_out[range.x + k] = (uint32_t)v;
-      }
-      __syncthreads();
-      continue;
-    }
-    const uint32_t np = GS_SORT_THREADS * R;
-    const uint32_t* segw = reinterpret_cast<const uint32_t*>(seg);  // (gaussian, depth) word pairs
-    uint32_t vmin = ~0u, vmax = 0u;
-    for (uint32_t k0 = tid; k0 < np; k0 += 8 * GS_SORT_THREADS) {  // 8 loads in flight per work-item
-      uint32_t d[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t k = k0 + j * GS_SORT_THREADS;
-        d[j] = k < n ? segw[2 * k + 1] : ~0u;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t k = k0 + j * GS_SORT_THREADS;
-        if (k < n) {
-          vmin = min(vmin, d[j]);
-          vmax = max(vmax, d[j]);
-        }
-        if (k < np) {
-          s_dep[k] = d[j];
-          s_slot[k] = (uint16_t)k;
-        }
-      }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      vmin = min(vmin, (uint32_t)__shfl_xor((int)vmin, off));
-      vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, off));
-    }
-    if (lane == 0) {
-      s_red[0][wave] = vmin;
-      s_red[1][wave] = vmax;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < GS_SORT_THREADS / 64; ++w) {
-      vmin = min(vmin, s_red[0][w]);
-      vmax = max(vmax, s_red[1][w]);
-    }
-    // depth bits of positive floats order like the floats: sort (min(d, max) - min) over the bits of
-    // max - min only (C2's 4..12 depths: 24 bits, 6 passes); padding (~0) clamps to max and, stable
-    // and last to begin with, stays behind the real maxima
-    vmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmin);
-    vmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)vmax);
-    const uint32_t nbits = vmax > vmin ? 32u - (uint32_t)__builtin_clz(vmax - vmin) : 0u;
-    uint32_t cur = 0;
-    for (uint32_t sh = 0; sh < nbits; sh += 4) {
-#ifdef GS_PROBE_SORT_PASSES
-      if (sh >= 4 * GS_PROBE_SORT_PASSES) continue;
-#endif
-      const uint32_t so = cur * capn, dof = (cur ^ 1u) * capn;
-      // counts: bytes of c[0] (digits 0-7) and c[1] (digits 8-15); R <= 33 < 256
-      unsigned long long c0 = 0, c1 = 0;
-#pragma unroll 8
-      for (uint32_t r = 0; r < R; ++r) {
-        const uint32_t d = ((min(s_dep[so + tid * R + r], vmax) - vmin) >> sh) & 15u;
-        const unsigned long long inc = 1ull << ((d & 7u) * 8u);
-        c0 += d < 8u ? inc : 0ull;
-        c1 += d < 8u ? 0ull : inc;
-      }
-#pragma unroll
-      for (uint32_t d = 0; d < 8; ++d) {
-        s_cnt[d * GS_SORT_THREADS + tid] = (uint16_t)((c0 >> (8u * d)) & 0xFFu);
-        s_cnt[(d + 8) * GS_SORT_THREADS + tid] = (uint16_t)((c1 >> (8u * d)) & 0xFFu);
-      }
-      __syncthreads();
-      // exclusive scan of the counters in (digit, work-item) order: work-item t holds entries [16t, 16t+16)
-      uint4* cw = reinterpret_cast<uint4*>(s_cnt + 16u * tid);
-      const uint4 a0 = cw[0], a1 = cw[1];
-      uint32_t v[16] = {a0.x & 0xFFFFu, a0.x >> 16, a0.y & 0xFFFFu, a0.y >> 16, a0.z & 0xFFFFu, a0.z >> 16,
-                        a0.w & 0xFFFFu, a0.w >> 16, a1.x & 0xFFFFu, a1.x >> 16, a1.y & 0xFFFFu, a1.y >> 16,
-                        a1.z & 0xFFFFu, a1.z >> 16, a1.w & 0xFFFFu, a1.w >> 16};
-      uint32_t sum = 0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t x = v[k];
-        v[k] = sum;
-        sum += x;
-      }
-      const uint32_t incl = wave_incl_scan(sum);
-      if (lane == 63) s_red[0][wave] = incl;
-      __syncthreads();
-      uint32_t base = incl - sum;
-      for (uint32_t w = 0; w < wave; ++w) base += s_red[0][w];
-      cw[0] = make_uint4((v[0] + base) | ((v[1] + base) << 16), (v[2] + base) | ((v[3] + base) << 16),
-                         (v[4] + base) | ((v[5] + base) << 16), (v[6] + base) | ((v[7] + base) << 16));
-      cw[1] = make_uint4((v[8] + base) | ((v[9] + base) << 16), (v[10] + base) | ((v[11] + base) << 16),
-                         (v[12] + base) | ((v[13] + base) << 16), (v[14] + base) | ((v[15] + base) << 16));
-      __syncthreads();
-      // scatter: stable inside the work-item (running byte counters), across work-items (the scan)
-      // (batches of 8: all loads of a batch issue before its stores, which the compiler may not
-      // reorder across: every array lives in the one LDS arena)
-      c0 = 0;
-      c1 = 0;
-      for (uint32_t r0 = 0; r0 < R; r0 += 8) {
-        uint32_t dv[8], sv[8], dst[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) {
-          const uint32_t p = tid * R + min(r0 + j, R - 1);
-          dv[j] = s_dep[so + p];
-          sv[j] = s_slot[so + p];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) {
-          const uint32_t d = ((min(dv[j], vmax) - vmin) >> sh) & 15u;
-          const uint32_t bit = (d & 7u) * 8u;
-          const unsigned long long cc = d < 8u ? c0 : c1;
-          const uint32_t local = (uint32_t)(cc >> bit) & 0xFFu;
-          const bool ok = r0 + j < R;
-          c0 += (ok && d < 8u) ? (1ull << bit) : 0ull;
-          c1 += (ok && d >= 8u) ? (1ull << bit) : 0ull;
-          dst[j] = (uint32_t)s_cnt[d * GS_SORT_THREADS + tid] + local;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-          if (r0 + j < R) {
-            s_dep[dof + dst[j]] = dv[j];
-            s_slot[dof + dst[j]] = (uint16_t)sv[j];
-          }
-      }
-      __syncthreads();
-      cur ^= 1u;
-    }
-    const uint32_t* sd = s_dep + cur * capn;
-    uint16_t* ss = s_slot + cur * capn;
-    // ties: equal depths in gaussian order
-    int tie = 0;
-    for (uint32_t k = tid; k + 1 < n; k += GS_SORT_THREADS) tie |= sd[k] == sd[k + 1];
-    if (__syncthreads_or(tie)) {
-      int changed;
-      do {
-        changed = 0;
-        for (uint32_t ph = 0; ph < 2; ++ph) {
-          for (uint32_t k = 2 * tid + ph; k + 1 < n; k += 2 * GS_SORT_THREADS)
-            if (sd[k] == sd[k + 1]) {
-              const uint16_t x = ss[k], y = ss[k + 1];
-              if (segw[2 * (uint32_t)y] < segw[2 * (uint32_t)x]) {
-                ss[k] = y;
-                ss[k + 1] = x;
-                changed = 1;
-              }
-            }
-          __syncthreads();
-        }
-      } while (__syncthreads_or(changed));
-    }
-    for (uint32_t k0 = tid; k0 < n; k0 += 8 * GS_SORT_THREADS) {  // 8 gathers in flight per work-item
-      uint32_t g[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t k = k0 + j * GS_SORT_THREADS;
-        g[j] = k < n ? segw[2 * (uint32_t)ss[k]] : 0u;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t k = k0 + j * GS_SORT_THREADS;
-        if (k < n) {
-          keys_out[range.x + k] = tbits | sd[k];
-          vals_out[range.x + k] = g[j];
-        }
       }
     }
     __syncthreads();  // LDS reused by the next tile
@@ -1203,11 +1226,20 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
           return e2;
         w->sort_attr = true;
       }
+      // tiles beyond the LDS capacity sort in a global scratch ([2][g_cap] u32 + [2][g_cap] u16 at the
+      // pair offsets), allocated once a frame has had such tiles
+      uint32_t g_cap = 0;
+      if (w->k_host[1] > GS_SORT_THREADS * GS_RADIX_MAXR) {
+        if ((e2 = ensure(w->sort_scratch, (size_t)cap * 12u))) return e2;
+        g_cap = (uint32_t)std::min<size_t>(w->sort_scratch.bytes / 12u, 0xFFFFFFFFu);
+      }
+      uint32_t* g_dep = g_cap ? (uint32_t*)w->sort_scratch.p : nullptr;
+      uint16_t* g_slot = g_cap ? (uint16_t*)(g_dep + 2 * (size_t)g_cap) : nullptr;
       hipLaunchKernelGGL(gs_sort_large_kernel, dim3(w->sort_grid), dim3(GS_SORT_THREADS), gs_radix_lds(w->sort_r), s,
-                       (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
-                       (const unsigned long long*)w->tile_slots.p, (const uint32_t*)w->large.p,
-                       (uint32_t*)w->large_ctr.p, (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p,
-                       (const uint32_t*)w->total.p, cap, w->sort_r);
+                         (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
+                         (const unsigned long long*)w->tile_slots.p, (const uint32_t*)w->large.p,
+                         (const uint32_t*)w->large_ctr.p, (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p,
+                         (const uint32_t*)w->total.p, cap, w->sort_r, g_dep, g_slot, g_cap);
       if ((e2 = hipGetLastError())) return e2;
     }
     if ((e2 = mark(4))) return e2;
@@ -1228,7 +1260,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = hipEventSynchronize(w->k_event))) return e;
   const uint32_t K = w->k_host[0];
   {  // the next frame's large-tile sort: LDS capacity from the largest tile of the previous frame
-     // (k_host[1]; +1/8 headroom), persistent workgroups from this frame's large-tile count (k_host[2])
+     // (k_host[1]; +1/8 headroom), workgroups from this frame's large-tile count (k_host[2])
     const uint32_t big = w->k_host[1] + w->k_host[1] / 8u;
     w->sort_r = std::min((uint32_t)GS_RADIX_MAXR, ((big + GS_SORT_THREADS - 1) / GS_SORT_THREADS) | 1u);
     w->sort_grid = std::max(64u, std::min(4096u, w->k_host[2] + w->k_host[2] / 4u));

@@ -67,11 +67,13 @@ def test_gaussians_parity(renderer, oracle_lib, n, W, H):
 
 @pytest.mark.parametrize("n,W,H", [(20000, 320, 180),      # tiles of 256-1000 pairs: in-blend and radix sorts
                                    (300000, 1920, 1080),   # C2 layout at 3x the density: thousands of large tiles
-                                   (3000, 48, 40)])        # ~3k pairs per tile
+                                   (3000, 48, 40),         # ~3k pairs per tile
+                                   (12000, 48, 40)])       # ~12k pairs per tile: beyond LDS, global-scratch radix
 def test_gaussians_large_tile_sorts(renderer, oracle_lib, n, W, H):
     """Tiles above 256 pairs: the first frame after a smaller one sorts them inside the blend (rank
-    counting up to 512, bitonic above), later frames in gs_sort_large_kernel (LDS radix sort) - both
-    must give the oracle's sorted keys / values bit for bit, including equal-depth ties."""
+    counting up to 512, bitonic above), later frames in gs_sort_large_kernel (radix sort in LDS, or
+    in a global scratch above 8448 pairs) - all must give the oracle's sorted keys / values bit for
+    bit, including equal-depth ties."""
     g = Y.gaussians_c2(n, seed=5)
     g["means"][1::97] = g["means"][0::97][: len(g["means"][1::97])]  # duplicated means: equal depths
     ubo = _gauss_ubo(W, H)
@@ -79,7 +81,7 @@ def test_gaussians_large_tile_sorts(renderer, oracle_lib, n, W, H):
     ref = oracle_lib.splat_gaussians(g, ubo, W, H)
     tiny = {k: _dev(v) for k, v in Y.gaussians_c2(10, seed=1).items()}
     renderer.splat_gaussians(tiny, ubo, W, H, torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"))
-    for frame in range(2):  # frame 0: after a small frame (in-blend sorts); frame 1: the radix kernel
+    for frame in range(3):  # frame 0: after a small frame (in-blend sorts); frames 1, 2: the radix kernel
         out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
         st = renderer.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
         torch.cuda.synchronize()
