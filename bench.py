@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-hybrid", action="store_true")
     ap.add_argument("--no-gpu-bvh", action="store_true")
     ap.add_argument("--no-gs-1m", action="store_true", help="skip the 1M-Gaussian splat and the point-cloud init legs")
+    ap.add_argument("--no-gs-10m", action="store_true", help="skip the 10M-Gaussian 3840x2160 splat leg (C5's splat)")
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
     ap.add_argument("--hybrid-spp", type=int, default=16)
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented counting pass")
@@ -258,7 +259,8 @@ def main():
             "value": round(N * world / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
             "workload": f"C2 3DGS forward: {N} synthetic Gaussians, {W}x{H}", "pairs_K": int(K),
             "stages_ms": {k: round(float(v), 4) for k, v in
-                          zip(["preprocess+count", "colscan", "scatter", "-", "-", "sort_blend"], stages) if k != "-"},
+                          zip(["preprocess+count", "colscan", "scatter", "sort_large", "-", "sort_blend"], stages)
+                          if k != "-"},
             "roofline": {"bound": "hbm", "kernel": "whole pipeline", "achieved": round(b_gs / (gms * 1e-3) / 1e9, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(b_gs / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "alg_bytes": b_gs},
@@ -293,6 +295,28 @@ def main():
             out["gs_init"] = {"workload": f"3DGS init from a {pts.shape[0]}-point cloud (exact 3-NN scales)",
                               "ms": round(di * 1e3, 3), "mpoints_per_s": round(pts.shape[0] / di / 1e6, 1)}
             del g1, pts, rgbp
+        # C5's splat on one GPU: 10M C2-distributed Gaussians at 3840x2160 (tiles up to ~28k pairs: the
+        # global-scratch radix path); the 8-GPU C5 shards these tile rows across ranks (dist.tile_row_shard)
+        if world == 1 and not args.no_gs_10m:
+            W5, H5, N5 = 3840, 2160, 10_000_000
+            g5 = {k: torch.from_numpy(v).cuda() for k, v in Y.gaussians_c2(N5, seed=5).items()}
+            img5 = torch.zeros((H5, W5, 4), dtype=torch.float32, device="cuda")
+            g5pose = Camera(aspect=W5 / H5).look_at([0.0, 0.0, 0.0], [0.0, 0.0, -1.0])
+            g5ubo = make_ubo(g5pose, cornell_box_scene(), 0)
+            for _ in range(3):  # the sort sizes follow the previous frames' tiles
+                r.splat_gaussians(g5, g5ubo, W5, H5, img5, stream=stream)
+            torch.cuda.synchronize()
+            n5 = 5
+            t0 = time.perf_counter()
+            for _ in range(n5):
+                r.splat_gaussians(g5, g5ubo, W5, H5, img5, stream=stream)
+            torch.cuda.synchronize()
+            d5 = (time.perf_counter() - t0) / n5
+            st5 = r.splat_gaussians(g5, g5ubo, W5, H5, img5, want_stats=True, stream=stream)
+            out["gs_10m_4k"] = {"workload": f"C5 splat on one GPU: {N5} C2-distributed Gaussians, {W5}x{H5}",
+                                "value": round(N5 / d5 / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(d5 * 1e3, 3),
+                                "pairs_K": int(st5.num_rendered)}
+            del g5, img5
         if args.no_pt:
             out.update({"value": out["gs"]["value"], "unit": "Gsplats/s", "ms_per_step": out["gs"]["ms_per_step"],
                         "config": {"workload": out["gs"]["workload"]}, "data": "synthetic Gaussians (seeded)"})

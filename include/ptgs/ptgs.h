@@ -372,7 +372,8 @@ int ptgs_splat_get_buffers(const ptgs_ctx* ctx, ptgs_splat_buffers* out);
 
 /* With PTGS_FLAG_TIME_STAGES: milliseconds of the stages of the most recent ptgs_splat_gaussians
  * call, measured with hipEvents on its stream: [0] preprocess + count (tile histograms) [1] column
- * scan (tile totals, K) [2] scatter (pairs into tile segments) [3] 0 [4] 0 [5] sort + blend. Synchronises. */
+ * scan (tile totals) [2] scatter (pairs into tile segments, K) [3] radix sort of the tiles above 512 pairs
+ * [4] 0 [5] sort (tiles up to 512 pairs) + blend. Synchronises. */
 int ptgs_splat_stage_ms(ptgs_ctx* ctx, float out_ms[6]);
 
 /* ---------------- dataset capture (Engine::captureSceneData, engine.cpp:2658-2814) -------- */

@@ -197,7 +197,8 @@ class Renderer:
         return b
 
     def splat_stage_ms(self) -> np.ndarray:
-        """[preprocess, count, scatter, 0, 0, sort+blend] ms of the last splat (FLAG_TIME_STAGES)."""
+        """[preprocess+count, colscan, scatter, large-tile sort, 0, sort+blend] ms of the last splat
+        (FLAG_TIME_STAGES)."""
         out = np.zeros(6, np.float32)
         self._chk(self.lib.ptgs_splat_stage_ms(self._h, _abi.fptr(out)), "ptgs_splat_stage_ms")
         return out

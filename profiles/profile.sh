@@ -8,7 +8,7 @@ set -euo pipefail
 TAG=${1:-r01}
 # only the headline legs (C3 path trace, C2 splat): every dispatch of a kernel is the same workload,
 # so the per-kernel averages are the per-launch figures bench.py reports
-ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-hybrid --no-gs-1m --no-gpu-bvh"}
+ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-hybrid --no-gs-1m --no-gs-10m --no-gpu-bvh"}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
