@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
     ap.add_argument("--hybrid-spp", type=int, default=16)
     ap.add_argument("--count-spp", type=int, default=4, help="spp of the instrumented counting pass")
+    ap.add_argument("--c5", action="store_true",
+                    help="also run BASELINE config 5 (10M Gaussians + 1M-tri mesh, 3840x2160, 256 spp in total: "
+                         "sample shard + RCCL all-reduce, splat-over composite by tile-row shard + reduce)")
     return ap.parse_args()
 
 
@@ -363,6 +366,63 @@ def main():
             "gsplats_per_s": round(args.hybrid_gaussians / hdt / 1e9, 4),
         }
         del haccum, hdepth, hdg
+
+    # ------------------------------------------------------------------ C5 (opt-in): the 8-GPU config
+    # 1M-tri atrium + 10M C2-distributed Gaussians in its camera frame, 3840x2160, 256 spp in total.
+    # Rank g traces samples g, g+N, ... (256/N each, SUM), one all-reduce of the radiance (every rank
+    # needs the frame under its splat rows), primary-hit depth, splat-over of its tile rows into a
+    # zeroed frame, one reduce of the disjoint composites to rank 0 (strong scaling).
+    if args.c5 and not args.no_pt:
+        from pathtracer_gaussiansplatting_amd import ACCUM_SUM as _SUM
+        from pathtracer_gaussiansplatting_amd import dist as D
+        W5, H5, T5, G5, SPP5 = 3840, 2160, 1_000_000, 10_000_000, 256
+        if SPP5 % world:
+            raise SystemExit("--c5 needs a world size dividing 256")
+        sc5 = Y.atrium_scene(target_tris=T5, seed=2)
+        sc5.blue_noise = Y.blue_noise(1024)
+        info5 = r.upload_scene(sc5)
+        pose5 = Camera(aspect=W5 / H5).look_at([-15.0, 4.0, 5.0], [10.0, 3.0, -3.0])
+        g5 = Y.gaussians_c2(G5, seed=5)
+        v5 = np.array(make_ubo(pose5, sc5, 0, height=H5).view, np.float64).reshape(4, 4).T
+        m5 = np.concatenate([g5["means"].astype(np.float64), np.ones((G5, 1))], 1)
+        g5["means"] = (m5 @ np.linalg.inv(v5).T)[:, :3].astype(np.float32)
+        dg5 = {k: torch.from_numpy(v).cuda() for k, v in g5.items()}
+        del g5, m5
+        acc5 = torch.zeros((H5, W5, 4), dtype=torch.float32, device="cuda")
+        dep5 = torch.zeros((H5, W5), dtype=torch.float32, device="cuda")
+        comp5 = torch.zeros((H5, W5, 4), dtype=torch.float32, device="cuda")
+        rows5 = D.tile_row_shard(rank, world, H5)
+
+        def c5_frame():
+            u5 = make_ubo(pose5, sc5, rank, ambient=(0.3, 0.4, 0.5, 1.0), height=H5)
+            acc5.zero_()
+            r.trace_camera(u5, W5, H5, acc5, spp=SPP5 // world, frame_stride=world, mode=_SUM, stream=stream)
+            D.all_reduce_sum(acc5)
+            mean5 = D.resolve_mean(acc5)
+            r.trace_depth(u5, W5, H5, dep5, stream=stream)
+            comp5.zero_()
+            if rows5[1] > rows5[0]:
+                r.splat_gaussians(dg5, u5, W5, H5, comp5, tile_rows=rows5, over=(dep5, mean5), stream=stream)
+            D.reduce_sum(comp5)
+
+        c5_frame()  # warm-up (sort sizes follow the previous frame's tiles)
+        torch.cuda.synchronize()
+        r.stats_reset(stream)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        c5_frame()
+        torch.cuda.synchronize()
+        barrier()
+        d5 = max_over_ranks(time.perf_counter() - t0)
+        s5 = r.stats()
+        rays5 = sum_over_ranks(float(s5.extension_rays + s5.shadow_rays))
+        out["c5"] = {"workload": f"C5: {G5} Gaussians + {int(info5.num_triangles)}-tri mesh, {W5}x{H5}, {SPP5} spp "
+                                 f"in total ({SPP5 // world} per GPU), sample shard + tile-row shard x{world}",
+                     "ms_per_frame": round(d5 * 1e3, 2), "mrays_per_s": round(rays5 / d5 / 1e6, 1),
+                     "gsplats_per_s": round(G5 / d5 / 1e9, 4), "scaling": "strong",
+                     "bvh_nodes": int(info5.num_bvh_nodes), "bvh_depth": int(info5.bvh_depth)}
+        del dg5, acc5, dep5, comp5
 
     # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_pt:
