@@ -238,25 +238,42 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   Hit h; h.t = r.tmax; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu; h.slot = 0;
   int sp = 0;
   int node = 0;
-  while (true) {
-    while (node >= 0) {
+  // while-while with postponed leaves (Aila & Laine 2009): a lane that reaches a leaf parks it and
+  // keeps walking interior nodes until every lane still in the loop holds a leaf, so the leaf phase
+  // runs with more lanes busy (+2% Mrays/s on C3, tools/ab_pt.py; packing the slab FMAs of child
+  // pairs into v_pk_fma_f32 measured -1.4%). The closest hit is the minimum over (t, gid) of every
+  // candidate, so visiting order changes neither the hit nor the image.
+  const int DONE = 0x7fffffff;
+  int leaf = DONE;
+  for (;;) {
+    while (node >= 0 && node != DONE) {
       Box4 b;
       box4(r, sc.nodes + 8 * node, h.t, b);
       if (STATS) cnt.nodes += 4;
       if (b.hits == 0) {
-        if (sp == 0) return h;
-        node = stack[(--sp) * PTGS_BLOCK];
-        continue;
+        node = sp ? stack[(--sp) * PTGS_BLOCK] : DONE;
+      } else {
+        cswap4(b, 0, 1); cswap4(b, 2, 3); cswap4(b, 0, 2); cswap4(b, 1, 3); cswap4(b, 1, 2);
+        if (b.hits > 3) stack[(sp++) * PTGS_BLOCK] = b.c[3];
+        if (b.hits > 2) stack[(sp++) * PTGS_BLOCK] = b.c[2];
+        if (b.hits > 1) stack[(sp++) * PTGS_BLOCK] = b.c[1];
+        node = b.c[0];
       }
-      cswap4(b, 0, 1); cswap4(b, 2, 3); cswap4(b, 0, 2); cswap4(b, 1, 3); cswap4(b, 1, 2);
-      if (b.hits > 3) stack[(sp++) * PTGS_BLOCK] = b.c[3];
-      if (b.hits > 2) stack[(sp++) * PTGS_BLOCK] = b.c[2];
-      if (b.hits > 1) stack[(sp++) * PTGS_BLOCK] = b.c[1];
-      node = b.c[0];
+      if (node < 0 && leaf == DONE) {
+        leaf = node;
+        node = sp ? stack[(--sp) * PTGS_BLOCK] : DONE;
+      }
+      if (__all(leaf != DONE || node == DONE)) break;
     }
-    leaf_closest<STATS, TEX>(sc, r, node, h, seed, cnt);
-    if (sp == 0) return h;
-    node = stack[(--sp) * PTGS_BLOCK];
+    if (leaf != DONE) {
+      leaf_closest<STATS, TEX>(sc, r, leaf, h, seed, cnt);
+      leaf = DONE;
+    }
+    if (node < 0) {
+      leaf_closest<STATS, TEX>(sc, r, node, h, seed, cnt);
+      node = sp ? stack[(--sp) * PTGS_BLOCK] : DONE;
+    }
+    if (node == DONE) return h;
   }
 }
 
