@@ -239,7 +239,9 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
 // Order inside a tile's segment depends on LDS atomic order and is fixed by the blend's per-tile sort.
 #define GS_BIN_THREADS 1024
 #define GS_MAX_CHUNKS 256    // colscan: 4 waves x 64 chunks
-#define GS_CHUNK_MIN 1024    // Gaussians per chunk (at least)
+#ifndef GS_CHUNK_MIN
+#define GS_CHUNK_MIN 512     // Gaussians per chunk (at least)
+#endif
 #define GS_BAND_TILES 8192   // max tiles per band (LDS: 32 KiB count, 64 KiB scatter); W <= 131072 px
 #define GS_TILE_SLOTS 256    // fixed key slots per tile (= the register-sort limit)
 #define GS_MAX_GROUPS 4096   // 64-tile groups (262144 tiles)
@@ -829,7 +831,10 @@ struct GStage {  // one staged blend record (see gs_preprocess_one)
 //           before the Gaussian that would take T below 1e-4 (the reference's rule).
 // OVER (hybrid composite): per-pixel depth limit and an "under" image instead of the background colour
 template <bool OVER>
-__global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, const uint2* __restrict__ ranges,
+#ifndef GS_BLEND_MIN_BLOCKS
+#define GS_BLEND_MIN_BLOCKS 8  // 64 VGPRs: 8 waves per SIMD (vs 7 at 70 VGPRs): +3% at C2
+#endif
+__global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_kernel(SplatCam cam, const uint2* __restrict__ ranges,
                                                                  unsigned long long* __restrict__ pairs,
                                                                  uint32_t sorted_above,
                                                                  unsigned long long* __restrict__ keys_out,
@@ -847,7 +852,9 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
   __shared__ __attribute__((aligned(16))) char s_arena[GS_ARENA_MIN];
   GStage* s_stage = reinterpret_cast<GStage*>(s_arena);
   uint32_t(*s_list)[GS_BLOCK + 4] = reinterpret_cast<uint32_t(*)[GS_BLOCK + 4]>(s_arena + sizeof(GStage) * (GS_BLOCK + 1));
-  __shared__ unsigned long long s_key[GS_MID];  // register-sort exchanges; a mid tile's sorted keys
+  // the register sort's 64 / 128 exchanges and a mid tile's ranked keys alias the arena: records are
+  // staged only after the last read of either (behind a barrier)
+  unsigned long long* s_key = reinterpret_cast<unsigned long long*>(s_arena);
   __shared__ uint8_t s_mask[GS_BLOCK];
   __shared__ uint32_t s_qcnt[4][4];  // [wave][quadrant]
   if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
@@ -919,6 +926,7 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_sort_blend_kernel(SplatCam cam, c
         const bool swap = (other < key) == (((tid & j) == 0) == ((tid & k) == 0));
         key = swap ? other : key;
       }
+    if (npad >= 128) __syncthreads();  // the last exchange reads are done before records overwrite them
     if (tid < n) {
       s_stage[tid].a = ra;
       s_stage[tid].b = rb;
