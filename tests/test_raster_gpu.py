@@ -93,6 +93,32 @@ def test_gaussians_large_tile_sorts(renderer, oracle_lib, n, W, H):
         assert err < 1e-4, (frame, err)
 
 
+def test_gaussians_beyond_24bit_indices(renderer, oracle_lib):
+    """2^24 + 3 Gaussians (the register sort packs the gaussian index in 24 bits): every tile goes
+    through the LDS rank-count / radix sorts instead; 3000 visible, the rest behind the camera."""
+    n, vis, W, H = (1 << 24) + 3, 3000, 160, 96
+    g = Y.gaussians_c2(vis, seed=9)
+    full = {}
+    for k, v in g.items():
+        a = np.zeros((n,) + v.shape[1:], np.float32)
+        a[:] = v[0]
+        a[-vis:] = v
+        full[k] = a
+    full["means"][:-vis, 2] = 5.0  # behind the camera (view looks down -Z): culled
+    ubo = _gauss_ubo(W, H)
+    dg = {k: _dev(v) for k, v in full.items()}
+    ref = oracle_lib.splat_gaussians(full, ubo, W, H)
+    out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    for _ in range(2):  # the second frame also sorts the tiles above 512 pairs in the radix kernel
+        st = renderer.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
+        torch.cuda.synchronize()
+        b = renderer.splat_buffers()
+        assert st.num_rendered == ref["K"]
+        np.testing.assert_array_equal(_read(renderer, b.sorted_keys, ref["K"], np.uint64), ref["keys"])
+        np.testing.assert_array_equal(_read(renderer, b.sorted_values, ref["K"], np.uint32), ref["vals"])
+        assert U.rel_l2(out.cpu().numpy(), ref["image"]) < 1e-4
+
+
 def test_gaussians_tile_row_shards_compose(renderer):
     """§8e screen-tile shard: rendering tile rows [0,a) and [a,gy) separately == the full frame."""
     n, W, H = 5000, 200, 120
