@@ -824,9 +824,10 @@ struct GStage {  // one staged blend record (see gs_preprocess_one)
 //           are streamed in batches of 256, the records of batch b + 1 (and the values of b + 2) in
 //           flight while batch b blends.
 //  blend    wave w shades the 8x8 quadrant q = w of the tile (x half w & 1, y half w >> 1), one pixel
-//           per lane. Each staged Gaussian's alpha box is tested against the four quadrants; a ballot
-//           + LDS offsets compact that into four ordered per-quadrant lists, so a wave iterates only
-//           the Gaussians that can touch its 64 pixels. alpha = min(0.99, 2^z) with the hardware exp2
+//           per lane. Each staged Gaussian's alpha box is tested against the four quadrants (a 4-bit
+//           mask in LDS); every wave ballots bit w over the batch's masks in sorted order into its own
+//           list (no cross-wave counts: one barrier per batch), so a wave iterates only the
+//           Gaussians that can touch its 64 pixels. alpha = min(0.99, 2^z) with the hardware exp2
 //           (within 1e-4 relative L2 of the oracle's exp, test_raster_gpu.py); front to back, stop
 //           before the Gaussian that would take T below 1e-4 (the reference's rule).
 // OVER (hybrid composite): per-pixel depth limit and an "under" image instead of the background colour
@@ -856,7 +857,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   // staged only after the last read of either (behind a barrier)
   unsigned long long* s_key = reinterpret_cast<unsigned long long*>(s_arena);
   __shared__ uint8_t s_mask[GS_BLOCK];
-  __shared__ uint32_t s_qcnt[4][4];  // [wave][quadrant]
+  __shared__ uint8_t s_sslot[GS_BLOCK];  // small tiles: staging slot of sorted position p
   if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   const uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
@@ -937,6 +938,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       vals_out[range.x + tid] = (uint32_t)(key >> 8) & 0xFFFFFFu;
 #endif
       my_slot = (uint32_t)key & 0xFFu;
+      s_sslot[tid] = (uint8_t)my_slot;
     }
   } else {
     if (mid) {
@@ -1005,22 +1007,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   const char* stage = reinterpret_cast<const char*>(s_stage);
   int todo = (int)n;
   for (uint32_t base = 0; todo > 0; base += GS_BLOCK, todo -= GS_BLOCK) {
-    // (small tiles: the barrier also publishes the records and masks staged after the sort; large
-    // tiles: the previous batch's lists have been consumed)
+    // (small tiles: the barrier also publishes the records, masks and sorted slots staged after the
+    // sort; large tiles: every wave is done with the previous batch)
     if (__syncthreads_count(done) == GS_BLOCK) break;
     const uint32_t idx = base + tid;
-    uint32_t m = 0, slot = tid;
-    if (small) {
-      if (idx < n) {
-        slot = my_slot;
-        m = s_mask[slot];
-      }
-    } else {
+    if (!small) {
       if (idx < n) {
         s_stage[tid].a = ra;
         s_stage[tid].b = rb;
         s_stage[tid].c = rc;
-        m = quad_mask(ra, rc);
+        s_mask[tid] = (uint8_t)quad_mask(ra, rc);
       }
       // next batch: its records (values loaded a batch ago) and the values of the one after
       if (idx + GS_BLOCK < n) {
@@ -1030,28 +1026,29 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         rc = rec[3 * g + 2];
       }
       if (idx + 2 * GS_BLOCK < n) g_next = vals_out[range.x + idx + 2 * GS_BLOCK];
+      __syncthreads();  // the batch's records and masks are staged
     }
-    uint32_t rank[4];
+    // each wave compacts its own quadrant's list from every staged mask, in sorted order (no
+    // cross-wave counts: one barrier per batch fewer, two fewer for a small tile)
+    const uint32_t nb = min((uint32_t)GS_BLOCK, n - base);
+    uint32_t cnt = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const unsigned long long bal = __ballot((m >> q) & 1u);
-      rank[q] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-      if (lane == 0) s_qcnt[wave][q] = (uint32_t)__popcll(bal);
+    for (uint32_t k = 0; k < GS_BLOCK / 64; ++k) {
+      const uint32_t p = k * 64u + lane;
+      const uint32_t slot = small ? (uint32_t)s_sslot[p] : p;
+      const bool bit = p < nb && ((s_mask[slot] >> wave) & 1u);
+      const unsigned long long bal = __ballot(bit);
+      if (bit)
+        s_list[wave][cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] =
+            slot * (uint32_t)sizeof(GStage);
+      cnt += (uint32_t)__popcll(bal);
     }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if ((m >> q) & 1u) {
-        uint32_t off = rank[q];
-        for (uint32_t w2 = 0; w2 < wave; ++w2) off += s_qcnt[w2][q];
-        s_list[q][off] = slot * (uint32_t)sizeof(GStage);
-      }
 #ifdef GS_PROBE_NO_EVAL
-    const uint32_t cnt = 0;
-#else
-    const uint32_t cnt = s_qcnt[0][wave] + s_qcnt[1][wave] + s_qcnt[2][wave] + s_qcnt[3][wave];
+    cnt = 0;
 #endif
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // wave-uniform trip count; the list is padded with the null Gaussian up to a multiple of 4
     const uint32_t cntu = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
     if (lane < 4) s_list[wave][cntu + lane] = GS_BLOCK * (uint32_t)sizeof(GStage);
