@@ -571,8 +571,12 @@ __device__ __forceinline__ void bitonic_flip_sort(uint32_t n, Swap swap_if) {
 //  publish  keys_out = tile << 32 | depth, vals_out = gaussian (the blend streams these)
 // A 16-byte-per-comparator LDS bitonic network measured ~5 MB of LDS traffic per 2.6k-pair tile
 // (LDS-bandwidth bound: ~130 us of the 1M-Gaussian frame); the radix moves ~0.2 MB.
+#ifndef GS_SORT_THREADS
 #define GS_SORT_THREADS 256
-#define GS_RADIX_MAXR 33      // items per work-item (odd) in LDS: up to 8448 keys
+#endif
+#ifndef GS_RADIX_MAXR
+#define GS_RADIX_MAXR (8448 / GS_SORT_THREADS)  // items per work-item in LDS: up to 8448 keys
+#endif
 #define GS_RADIX_MAXN 65535u  // u16 positions: global bitonic above (never met by the configs)
 
 __host__ __device__ constexpr size_t gs_radix_lds(uint32_t rmax) {
