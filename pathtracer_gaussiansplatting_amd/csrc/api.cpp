@@ -6,6 +6,9 @@
 //   recordCommandBuffer's vkCmdTraceRaysKHR :1971-1976 + rt_output_image running mean
 //       -> ptgs_trace_camera
 //   torus trace :1893-1900 / :2787-2794 -> ptgs_trace_torus
+#ifndef PTGS_BVH_LEAF
+#define PTGS_BVH_LEAF 4
+#endif
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -304,7 +307,7 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
   if (!built) {
     auto t0 = std::chrono::steady_clock::now();
     BvhOut bvh;
-    build_bvh(tris, 4, PTGS_STACK - 1, bvh);
+    build_bvh(tris, PTGS_BVH_LEAF, PTGS_STACK - 1, bvh);
     auto t1 = std::chrono::steady_clock::now();
     if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
     {

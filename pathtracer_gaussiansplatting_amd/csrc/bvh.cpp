@@ -6,6 +6,10 @@
 #include <cstring>
 #include <limits>
 
+#ifndef PTGS_BVH_CT
+#define PTGS_BVH_CT 0.125f
+#endif
+
 namespace ptgs {
 
 namespace {
@@ -114,7 +118,7 @@ struct Builder {
       }
       if (best_axis >= 0) {
         float leaf_cost = out_box.area() * n;
-        float split_cost = 0.125f * out_box.area() + best_cost;  // traversal step ~ 1/8 tri test
+        float split_cost = PTGS_BVH_CT * out_box.area() + best_cost;  // traversal step vs tri test
         if (n <= (uint32_t)max_leaf && leaf_cost <= split_cost && d > 0) return make_leaf(begin, n);
         float scale = NB / ext[best_axis];
         float lo = cb.lo[best_axis];

@@ -287,7 +287,8 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
       Box4 b;
       box4(r, sc.nodes + 8 * node, r.tmax, b);
       if (STATS) cnt.nodes += 4;
-      // order is irrelevant for an any-hit query: enter the first hit child, push the others
+      // order is irrelevant for an any-hit query: enter the first hit child, push the others (the
+      // closest-hit near-to-far order measured -9% for the shadow rays)
       int next = -0x7fffffff - 1;
       bool have = false;
 #pragma unroll
