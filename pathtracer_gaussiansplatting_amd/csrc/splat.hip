@@ -877,6 +877,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     return (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
            ((uint32_t)(xr && yb) << 3);
   };
+  // stage a record as the quadratic in tile-local pixel coordinates (ux, uy):
+  // z = A ux^2 + B ux uy + C uy^2 + D ux + E uy + F (five FMAs per evaluation instead of seven)
+  auto stage_rec = [&](uint32_t slot, const float4& ga, const float4& gb, const float4& gc) {
+    const float gx = ga.x - tx0, gy = ga.y - ty0, A = ga.z, B = ga.w, C = gb.x;
+    const float D = -2.0f * A * gx - B * gy, E = -B * gx - 2.0f * C * gy;
+    const float F = ((A * gx * gx + B * gx * gy) + C * gy * gy) + gb.y;
+    s_stage[slot].a = make_float4(A, B, C, D);
+    s_stage[slot].b = make_float4(E, F, gb.z, gb.w);
+    s_stage[slot].c = gc;
+  };
   // the tile's slot row is loaded together with its range (no dependent round trip for small tiles)
 #ifdef GS_PROBE_SLOT_N
   const uint2 range = ranges[tile];
@@ -934,9 +944,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       }
     if (npad >= 128) __syncthreads();  // the last exchange reads are done before records overwrite them
     if (tid < n) {
-      s_stage[tid].a = ra;
-      s_stage[tid].b = rb;
-      s_stage[tid].c = rc;
+      stage_rec(tid, ra, rb, rc);
       s_mask[tid] = (uint8_t)quad_mask(ra, rc);
 #ifndef GS_PROBE_NO_PUBLISH
       keys_out[range.x + tid] = tbits | (key >> 32);
@@ -1006,6 +1014,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   const bool inside = px < cam.W && py < cam.H;
   bool done = !inside;
   const float pfx = (float)px, pfy = (float)py;
+  const float ux = pfx - tx0, uy = pfy - ty0, uxx = ux * ux, uxy = ux * uy, uyy = uy * uy;
   const float lim = (OVER && inside) ? depth_lim[(size_t)py * cam.W + px] : 0.0f;
   float T = 1.0f;
   float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
@@ -1018,9 +1027,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const uint32_t idx = base + tid;
     if (!small) {
       if (idx < n) {
-        s_stage[tid].a = ra;
-        s_stage[tid].b = rb;
-        s_stage[tid].c = rc;
+        stage_rec(tid, ra, rb, rc);
         s_mask[tid] = (uint8_t)quad_mask(ra, rc);
       }
       // next batch: its records (values loaded a batch ago) and the values of the one after
@@ -1071,11 +1078,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
           const float gd = *reinterpret_cast<const float*>(stage + o + 44);
           done = done || !(gd < lim);
         }
-        const float dx = a.x - pfx, dy = a.y - pfy;
-        // z = A dx^2 + B dx dy + C dy^2 + log2 o. (The reference's power > 0 skip is not tested: the
-        // conic is positive definite (+0.3 low-pass), so power <= 0 up to rounding at power ~ 0.)
-        const float q2 = __builtin_fmaf(b.x * dy, dy, b.y);
-        const float z = __builtin_fmaf(__builtin_fmaf(a.z, dx, a.w * dy), dx, q2);
+        // z = A dx^2 + B dx dy + C dy^2 + log2 o as staged: a quadratic in the tile-local (ux, uy), five
+        // FMAs (the centre-relative form costs seven; the expansion's rounding is ~1e-6 in z). (The
+        // reference's power > 0 skip is not tested: the conic is positive definite (+0.3 low-pass),
+        // so power <= 0 up to rounding at power ~ 0.)
+        const float z = __builtin_fmaf(a.x, uxx, __builtin_fmaf(a.y, uxy, __builtin_fmaf(a.z, uyy,
+                                       __builtin_fmaf(a.w, ux, __builtin_fmaf(b.x, uy, b.y)))));
         const bool valid = !done && z >= -7.9943534f;  // alpha >= 1/255: z >= log2(1/255)
         const float alpha = valid ? fminf(0.99f, __builtin_amdgcn_exp2f(z)) : 0.0f;
         float wgt = alpha * T;
