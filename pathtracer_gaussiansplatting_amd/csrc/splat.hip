@@ -520,16 +520,6 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
   });
 }
 
-// recompute the (clamped) rect of a visible Gaussian — same integer math as preprocess
-__device__ __forceinline__ void gs_rect(const SplatCam& cam, float2 p, int r, int& x0, int& y0, int& x1, int& y1) {
-  x0 = min((int)cam.grid_x, max(0, (int)((p.x - (float)r) / (float)GS_BLOCK_X)));
-  y0 = min((int)cam.grid_y, max(0, (int)((p.y - (float)r) / (float)GS_BLOCK_Y)));
-  x1 = min((int)cam.grid_x, max(0, (int)((p.x + (float)r + (float)(GS_BLOCK_X - 1)) / (float)GS_BLOCK_X)));
-  y1 = min((int)cam.grid_y, max(0, (int)((p.y + (float)r + (float)(GS_BLOCK_Y - 1)) / (float)GS_BLOCK_Y)));
-  y0 = max(y0, (int)cam.row_begin);
-  y1 = min(y1, (int)cam.row_end);
-}
-
 // ascending bitonic sort ("flip" network: every comparator puts the min at the lower index) over
 // n elements; indices >= n act as +inf and are never touched, so n need not be a power of two.
 template <typename Swap>
@@ -810,7 +800,7 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
 }
 
 // ---- blend ----------------------------------------------------------------------------------------
-#define GS_ARENA_MIN (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)
+#define GS_ARENA (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)  // staged records + per-quadrant lists
 #define GS_MID 512  // tiles of (256, GS_MID] pairs are sorted inside the blend (rank counting)
 
 struct GStage {  // one staged blend record (see gs_preprocess_one)
@@ -855,7 +845,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
                                                                  float4* __restrict__ out) {
   // staged records of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads the
   // per-quadrant lists to a multiple of 4.
-  __shared__ __attribute__((aligned(16))) char s_arena[GS_ARENA_MIN];
+  __shared__ __attribute__((aligned(16))) char s_arena[GS_ARENA];
   GStage* s_stage = reinterpret_cast<GStage*>(s_arena);
   uint32_t(*s_list)[GS_BLOCK + 4] = reinterpret_cast<uint32_t(*)[GS_BLOCK + 4]>(s_arena + sizeof(GStage) * (GS_BLOCK + 1));
   // the register sort's 64 / 128 exchanges and a mid tile's ranked keys alias the arena: records are
