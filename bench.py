@@ -70,13 +70,28 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local)
+    # (local % device count: lets a 1-GPU box rehearse several ranks with BENCH_DIST_BACKEND=gloo;
+    # one rank per GPU otherwise)
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def reduce_to_root(t):
+        # RCCL reduce(SUM) to rank 0; the gloo rehearsal has no CUDA reduce: all-reduce instead
+        if world > 1:
+            if dist.get_backend() == "nccl":
+                dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
 
     def max_over_ranks(x: float) -> float:
         if world == 1:
@@ -97,7 +112,7 @@ def main():
     from pathtracer_gaussiansplatting_amd import synthetic as Y
 
     W, H, SPP = args.width, args.height, args.spp
-    r = Renderer(local)
+    r = Renderer(dev)
     stream = torch.cuda.current_stream()
     out = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f32"}
@@ -123,8 +138,7 @@ def main():
             r.trace_camera(ubo, W, H, accum, spp=SPP, frame_stride=world, mode=mode, stream=stream)
             if ev1 is not None:
                 ev1.record(stream)
-            if world > 1:
-                dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)
+            reduce_to_root(accum)
             frame_base += SPP
 
         for _ in range(args.warmup):
@@ -269,6 +283,30 @@ def main():
                          "frac": round(b_gs / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "alg_bytes": b_gs},
         }
         out["gs"]["splat_pairs_per_s"] = round(K * world / (gdt / gsteps) / 1e9, 4)  # (Gaussian, tile) instances, G/s
+        # two frames in flight (the reference's MAX_FRAMES_IN_FLIGHT = 2): consecutive frames alternate
+        # between two contexts on two streams, so one frame's front end overlaps the other's blend
+        r2 = Renderer(dev)
+        s2 = torch.cuda.Stream()
+        img2 = torch.zeros_like(img)
+        pipes = [(r, stream, img), (r2, s2, img2)]
+        for k in range(4):
+            rk, sk, ik = pipes[k % 2]
+            rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(gsteps):
+            rk, sk, ik = pipes[k % 2]
+            rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
+        torch.cuda.synchronize()
+        barrier()
+        g2dt = max_over_ranks(time.perf_counter() - t0)
+        out["gs"]["two_in_flight"] = {"value": round(N * world / (g2dt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
+                                      "ms_per_step": round(g2dt / gsteps * 1e3, 4),
+                                      "note": "same frames, alternating between two contexts / streams"}
+        r2.close()
+        del img2
         del dg
         # the same forward at the C4 hybrid's Gaussian count (1M), splat only
         if world == 1 and not args.no_gs_1m:
@@ -403,7 +441,7 @@ def main():
             comp5.zero_()
             if rows5[1] > rows5[0]:
                 r.splat_gaussians(dg5, u5, W5, H5, comp5, tile_rows=rows5, over=(dep5, mean5), stream=stream)
-            D.reduce_sum(comp5)
+            reduce_to_root(comp5)
 
         c5_frame()  # warm-up (sort sizes follow the previous frame's tiles)
         torch.cuda.synchronize()
