@@ -222,6 +222,7 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
 
   // gather triangles in flattening order (gid), skipping meshes with < 3 indices (engine.cpp:545-547)
   std::vector<BuildTri> tris;
+  std::vector<uint32_t> hitrec;  // per gid: global vertex indices + material (closest_hit's one fetch)
   bool has_transparent = false;
   for (uint32_t m = 0; m < d->num_meshes; ++m) {
     const ptgs_mesh_info& mi = d->meshes[m];
@@ -239,7 +240,9 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
         if (vi >= d->num_vertices) return fail(c, PTGS_EINVAL, "mesh %u prim %u: vertex %u out of range", m, p, vi);
         float* dst = k == 0 ? t.v0 : (k == 1 ? t.v1 : t.v2);
         std::memcpy(dst, d->vertices[vi].pos, 12);
+        hitrec.push_back(vi);
       }
+      hitrec.push_back(mi.material_index);
       t.mesh = m; t.prim = p; t.gid = (uint32_t)tris.size(); t.flags = flags;
       tris.push_back(t);
     }
@@ -334,6 +337,12 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
   if ((rc = upload(c, d->num_indices ? d->indices : &dummy_i, d->num_indices ? d->num_indices : 1, &s.indices))) return rc;
   if ((rc = upload(c, d->num_meshes ? d->meshes : &dummy_m, d->num_meshes ? d->num_meshes : 1, &s.meshes))) return rc;
   if ((rc = upload(c, d->materials, d->num_materials, &s.materials))) return rc;
+  {
+    const uint32_t zero4[4] = {0, 0, 0, 0};
+    if ((rc = upload(c, (const uint4*)(hitrec.empty() ? zero4 : hitrec.data()), hitrec.empty() ? 1 : hitrec.size() / 4,
+                     &s.hitrec)))
+      return rc;
+  }
   if ((rc = upload(c, d->light_triangles, d->num_light_triangles, &s.light_tris))) return rc;
   if ((rc = upload(c, d->light_cdf, d->num_light_cdf, &s.light_cdf))) return rc;
   if ((rc = upload(c, d->punctual_lights, d->num_punctual_lights, &s.plights))) return rc;

@@ -27,18 +27,13 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
   const DevScene& sc = *c.sc;
   const CamParams& cp = *c.cp;
 
-  const float4* rec = sc.tris + 3u * hit.slot;
-  uint32_t mesh = f2u(rec[0].w);
-  uint32_t prim = f2u(rec[1].w);
-  const ptgs_mesh_info info = sc.meshes[mesh];
-  const ptgs_material& mat = sc.materials[info.material_index];
-
-  uint32_t i0 = sc.indices[info.index_offset + prim * 3u + 0u];
-  uint32_t i1 = sc.indices[info.index_offset + prim * 3u + 1u];
-  uint32_t i2 = sc.indices[info.index_offset + prim * 3u + 2u];
-  const ptgs_vertex& v0 = sc.vertices[info.vertex_offset + i0];
-  const ptgs_vertex& v1 = sc.vertices[info.vertex_offset + i1];
-  const ptgs_vertex& v2 = sc.vertices[info.vertex_offset + i2];
+  // one 16-B fetch by gid replaces the triangle record -> MeshInfo -> indices chain (three dependent
+  // round trips): the same vertex / material indices, precomputed at upload
+  const uint4 hr = sc.hitrec[hit.gid];
+  const ptgs_material& mat = sc.materials[hr.w];
+  const ptgs_vertex& v0 = sc.vertices[hr.x];
+  const ptgs_vertex& v1 = sc.vertices[hr.y];
+  const ptgs_vertex& v2 = sc.vertices[hr.z];
 
   // :336-346
   float bx = (1.0f - hit.u) - hit.v, by = hit.u, bz = hit.v;
