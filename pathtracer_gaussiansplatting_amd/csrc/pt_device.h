@@ -257,23 +257,26 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   // candidate, so visiting order changes neither the hit nor the image.
   const int DONE = 0x7fffffff;
   int leaf = DONE;
+  auto push = [&](int x) { stack[(sp++) * PTGS_BLOCK] = x; };
+  auto pop = [&]() -> int { return sp ? stack[(--sp) * PTGS_BLOCK] : DONE; };
+  // (a register-cached stack top that hides the LDS read behind the node fetch measured -0.8%)
   for (;;) {
     while (node >= 0 && node != DONE) {
       Box4 b;
       box4(r, sc.nodes + 8 * node, h.t, b);
       if (STATS) cnt.nodes += 4;
       if (b.hits == 0) {
-        node = sp ? stack[(--sp) * PTGS_BLOCK] : DONE;
+        node = pop();
       } else {
         cswap4(b, 0, 1); cswap4(b, 2, 3); cswap4(b, 0, 2); cswap4(b, 1, 3); cswap4(b, 1, 2);
-        if (b.hits > 3) stack[(sp++) * PTGS_BLOCK] = b.c[3];
-        if (b.hits > 2) stack[(sp++) * PTGS_BLOCK] = b.c[2];
-        if (b.hits > 1) stack[(sp++) * PTGS_BLOCK] = b.c[1];
+        if (b.hits > 3) push(b.c[3]);
+        if (b.hits > 2) push(b.c[2]);
+        if (b.hits > 1) push(b.c[1]);
         node = b.c[0];
       }
       if (node < 0 && leaf == DONE) {
         leaf = node;
-        node = sp ? stack[(--sp) * PTGS_BLOCK] : DONE;
+        node = pop();
       }
       if (__all(leaf != DONE || node == DONE)) break;
     }
@@ -283,7 +286,7 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
     }
     if (node < 0) {
       leaf_closest<STATS, TEX>(sc, r, node, h, seed, cnt);
-      node = sp ? stack[(--sp) * PTGS_BLOCK] : DONE;
+      node = pop();
     }
     if (node == DONE) return h;
   }
@@ -541,6 +544,7 @@ __device__ void sample_emissive(ShadeCtx& c, const Payload& p, bool sg, v3 hit_p
   uint32_t idx = cdf_search(sc.light_cdf, num, r_select);
   uint32_t tri_idx = sc.light_cdf[idx].triangle_index;
   ptgs_light_triangle tri = sc.light_tris[tri_idx];
+  const uint32_t light_mat = tri.material_index;
   v3 p0 = ld3(sc.vertices[tri.v0].pos);
   v3 p1 = ld3(sc.vertices[tri.v1].pos);
   v3 p2 = ld3(sc.vertices[tri.v2].pos);
@@ -563,7 +567,7 @@ __device__ void sample_emissive(ShadeCtx& c, const Payload& p, bool sg, v3 hit_p
     float vis = trace_shadow<STATS, TEX>(c, so, lp, p.seed, cnt);
     vis = fmaxx(vis, transmission);
     if (vis > 0.0f) {
-      const ptgs_material& lm = sc.materials[tri.material_index];
+      const ptgs_material& lm = sc.materials[light_mat];
       v3 le = ld3(lm.emissive_factor_and_pad);
       float es = fmaxx(le.x, fmaxx(le.y, le.z));
       float pdf_nee = (es / c.cp->emissive_flux) * (dist_sq / ldn);
