@@ -168,8 +168,16 @@ struct Model {
   View view(int acc_index, size_t default_stride, size_t elem_bytes, const char* what) const {
     const JVal* acc = arr_at(doc, "accessors", acc_index);
     if (!acc) fail(std::string(what) + ": accessor index out of range");
+    // count / offsets / stride are untrusted JSON numbers: anything but an integer in [0, 2^32) is
+    // rejected before the cast (a double -> size_t cast of a negative or huge value is UB)
+    auto size_field = [&](const JVal* j) -> size_t {
+      const double d = ptgs::jdouble(j, 0);
+      if (!(d >= 0.0 && d < 4294967296.0) || d != (double)(uint64_t)d)
+        fail(std::string(what) + ": accessor count/offset/stride is not an integer in [0, 2^32)");
+      return (size_t)d;
+    };
     View v;
-    v.count = (size_t)ptgs::jdouble(acc->get("count"), 0);
+    v.count = size_field(acc->get("count"));
     v.ctype = ptgs::jint(acc->get("componentType"), 0);
     int bvi = ptgs::jint(acc->get("bufferView"), -1);
     if (bvi < 0) fail(std::string(what) + ": accessor without bufferView (sparse-only accessors unsupported)");
@@ -177,13 +185,17 @@ struct Model {
     if (!bv) fail(std::string(what) + ": bufferView index out of range");
     int bi = ptgs::jint(bv->get("buffer"), -1);
     if (bi < 0 || (size_t)bi >= buffers.size()) fail(std::string(what) + ": buffer index out of range");
-    size_t off = (size_t)ptgs::jdouble(bv->get("byteOffset"), 0) + (size_t)ptgs::jdouble(acc->get("byteOffset"), 0);
-    size_t bvstride = (size_t)ptgs::jdouble(bv->get("byteStride"), 0);
+    size_t off = size_field(bv->get("byteOffset")) + size_field(acc->get("byteOffset"));
+    size_t bvstride = size_field(bv->get("byteStride"));
     size_t tight = (size_t)comp_size(v.ctype) * type_count(ptgs::jstr(acc->get("type"), ""));
     v.stride = bvstride ? bvstride : (default_stride ? default_stride : tight);
     const std::vector<uint8_t>& buf = buffers[bi];
-    if (v.count && (off > buf.size() || (v.count - 1) * v.stride + elem_bytes > buf.size() - off))
-      fail(std::string(what) + ": accessor reads past the end of its buffer");
+    // overflow-free form of off + (count - 1) * stride + elem_bytes <= size
+    if (v.count) {
+      bool ok = off <= buf.size() && elem_bytes <= buf.size() - off;
+      if (ok && v.count > 1 && v.stride) ok = (v.count - 1) <= (buf.size() - off - elem_bytes) / v.stride;
+      if (!ok) fail(std::string(what) + ": accessor reads past the end of its buffer");
+    }
     v.p = buf.data() + off;
     return v;
   }
@@ -852,7 +864,19 @@ void load_gltf(const std::string& path, uint32_t flags, ptgs_scene_builder::Obje
     auto work = [&]() {
       for (size_t i; (i = next.fetch_add(1)) < jobs.size();) {
         Job& jb = jobs[i];
-        if (jb.ok) jb.ok = ptgs::decode_image_rgba8(jb.bytes.data(), jb.bytes.size(), jb.img, jb.err);
+        // no exception may leave a worker thread (std::terminate would abort the host process)
+        try {
+          if (jb.ok) jb.ok = ptgs::decode_image_rgba8(jb.bytes.data(), jb.bytes.size(), jb.img, jb.err);
+        } catch (const std::bad_alloc&) {
+          jb.ok = false;
+          jb.err = "out of memory decoding the image";
+        } catch (const std::exception& ex) {
+          jb.ok = false;
+          jb.err = ex.what();
+        } catch (...) {
+          jb.ok = false;
+          jb.err = "image decode failed";
+        }
         std::vector<uint8_t>().swap(jb.bytes);
       }
     };

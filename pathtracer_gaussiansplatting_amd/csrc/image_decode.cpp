@@ -208,6 +208,10 @@ bool decode_png(const uint8_t* d, size_t n, DecodedImage& out, std::string& err,
     ph[p] = H.h > (uint32_t)y0 ? (H.h - y0 + dy - 1) / dy : 0;
     if (pw[p] && ph[p]) need += (size_t)ph[p] * (png_row_bytes(pw[p], H) + 1);
   }
+  // bound the allocations by what the file can hold before making them: at most 2^28 pixels (as the
+  // JPEG path), and deflate expands at most ~1032:1, so a short IDAT cannot describe a huge image
+  if ((uint64_t)H.w * H.h > (1ull << 28)) { err = "PNG: image too large"; return false; }
+  if (need > idat.size() * (size_t)1040 + 4096) { err = "PNG: not enough pixel data"; return false; }
   std::vector<uint8_t> raw(need);
   {
     z_stream zs;

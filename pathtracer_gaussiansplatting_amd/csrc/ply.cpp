@@ -5,6 +5,7 @@
 // [0, 1] scaled by 255 and rounded); a trained-3DGS file without rgb gives colours from its SH DC
 // term f_dc_0..2 (0.5 + C0 * f_dc, clamped). Elements before "vertex" must have fixed-size rows in
 // binary files (list properties are only skippable in ASCII).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -123,6 +124,27 @@ extern "C" int ptgs_read_ply(const char* path, float* xyz, float* normals, uint8
   if (vi < 0) return PTGS_EIO;
   const Elem& V = elems[vi];
   if (V.count > 0xFFFFFFFFull) return PTGS_ERANGE;
+  // header counts must fit the body (checked before the count query returns, so a caller never
+  // sizes buffers from an impossible count): ASCII rows take at least one byte each, binary rows
+  // exactly their size (elements before "vertex" must have fixed-size rows)
+  const uint64_t body = bytes.size() - std::min(hdr_end, bytes.size());
+  size_t vert_off = hdr_end, vert_rs = 0;
+  if (ascii) {
+    for (int e = 0; e <= vi; ++e)
+      if (elems[e].count > body) return PTGS_EIO;
+  } else {
+    for (int e = 0; e <= vi; ++e) {
+      size_t rs = 0;
+      for (const Prop& pr : elems[e].props) {
+        if (pr.list) return PTGS_EIO;  // variable-size rows: unsupported in binary
+        rs += (size_t)pr.size;
+      }
+      const size_t left = bytes.size() - std::min(vert_off, bytes.size());
+      if (rs && elems[e].count > left / rs) return PTGS_EIO;  // (overflow-free)
+      if (e == vi) vert_rs = rs;
+      else vert_off += rs * elems[e].count;
+    }
+  }
   *count = (uint32_t)V.count;
   if (!xyz && !normals && !rgb) return PTGS_OK;
   if (capacity < V.count) return PTGS_ERANGE;
@@ -151,20 +173,23 @@ extern "C" int ptgs_read_ply(const char* path, float* xyz, float* normals, uint8
     }
   };
   if (ascii) {
+    // strtod / strtol stop at the terminating NUL, never past the buffer
+    bytes.push_back('\0');
     const char* p = (const char*)bytes.data() + hdr_end;
-    const char* end = (const char*)bytes.data() + bytes.size();
+    const char* end = (const char*)bytes.data() + bytes.size() - 1;
     auto next_line = [&]() {
       while (p < end && *p != '\n') ++p;
       if (p < end) ++p;
     };
     for (int e = 0; e < vi; ++e)
-      for (uint64_t r = 0; r < elems[e].count; ++r) next_line();
+      for (uint64_t r = 0; r < elems[e].count && p < end; ++r) next_line();
     for (uint64_t i = 0; i < V.count; ++i) {
+      if (p >= end) return PTGS_EIO;  // fewer rows than the header's vertex count
       for (size_t k = 0; k < V.props.size(); ++k) {
         char* q = nullptr;
         if (V.props[k].list) {  // count then items
           long cnt = strtol(p, &q, 10);
-          if (q == p) return PTGS_EIO;
+          if (q == p || cnt < 0) return PTGS_EIO;
           p = q;
           for (long t = 0; t < cnt; ++t) { strtod(p, &q); if (q == p) return PTGS_EIO; p = q; }
           row[k] = 0;
@@ -179,21 +204,7 @@ extern "C" int ptgs_read_ply(const char* path, float* xyz, float* normals, uint8
     }
     return PTGS_OK;
   }
-  size_t off = hdr_end;
-  for (int e = 0; e < vi; ++e) {
-    size_t rs = 0;
-    for (const Prop& pr : elems[e].props) {
-      if (pr.list) return PTGS_EIO;  // variable-size rows before the vertices: unsupported in binary
-      rs += (size_t)pr.size;
-    }
-    off += rs * elems[e].count;
-  }
-  size_t rs = 0;
-  for (const Prop& pr : V.props) {
-    if (pr.list) return PTGS_EIO;
-    rs += (size_t)pr.size;
-  }
-  if (off > bytes.size() || (bytes.size() - off) / rs < V.count) return PTGS_EIO;
+  const size_t off = vert_off, rs = vert_rs;
   for (uint64_t i = 0; i < V.count; ++i) {
     const uint8_t* q = bytes.data() + off + i * rs;
     for (size_t k = 0; k < V.props.size(); ++k) {
