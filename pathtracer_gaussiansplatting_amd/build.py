@@ -24,6 +24,10 @@ SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "capture.cpp", "comm.cpp", "jpeg
            "pt_kernels.hip", "raster.hip", "splat.hip", "knn.hip", "gltf.cpp", "image_decode.cpp", "ply.cpp"]
 # pure host code (scene ingest): plain g++, no device pass
 HOST_SOURCES = {"gltf.cpp", "image_decode.cpp", "ply.cpp"}
+# per-source extra flags. pt_kernels.hip: SimplifyCFG's common-store sinking merges stores to
+# different Payload fields from the branches of closest_hit into one store through a phi of
+# addresses, which SROA cannot split: the payload then stays a private (scratch) object.
+EXTRA = {"pt_kernels.hip": ["-mllvm", "-simplifycfg-sink-common=false"]}
 ARCH = os.environ.get("PTGS_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC]
@@ -44,7 +48,7 @@ def _compile(src: str, defines: tuple = (), build_dir: str = BUILD) -> str:
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj
     dflags = [f"-D{d}" for d in defines]
-    cmd = [_hipcc()] + COMMON + dflags + [f"--offload-arch={ARCH}", "-c", path, "-o", obj]
+    cmd = [_hipcc()] + COMMON + dflags + EXTRA.get(src, []) + [f"--offload-arch={ARCH}", "-c", path, "-o", obj]
     if src in HOST_SOURCES:
         cmd = ["g++"] + COMMON + dflags + ["-c", path, "-o", obj]
     elif src.endswith(".cpp"):

@@ -29,6 +29,9 @@ struct v4 { float x, y, z, w; };
 PTGS_HD v2 mk2(float x, float y) { v2 r; r.x = x; r.y = y; return r; }
 PTGS_HD v3 mk3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
 PTGS_HD v3 mk3(float s) { return mk3(s, s, s); }
+// component-wise c ? a : b (a ?: between two v3 values can lower to a select between two stack
+// copies: a dynamically addressed private object, i.e. scratch traffic in the path-tracer kernel)
+PTGS_HD v3 sel3(bool c, v3 a, v3 b) { return mk3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 PTGS_HD v4 mk4(float x, float y, float z, float w) { v4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
 
 PTGS_HD v3 operator+(v3 a, v3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }

@@ -374,7 +374,7 @@ __device__ __forceinline__ float blue_noise_dim(const Payload& p, int dim) {
 
 __device__ __forceinline__ v3 safe_normalize(v3 v) {
   float len = length3(v);
-  return (len < 1e-6f) ? mk3(0.0f, 1.0f, 0.0f) : v / len;
+  return sel3(len < 1e-6f, mk3(0.0f, 1.0f, 0.0f), v / len);
 }
 
 // closesthit.rchit:49-51
@@ -385,7 +385,7 @@ __device__ __forceinline__ v3 f_schlick(float cos_theta, v3 f0) {
 
 // :54-58
 __device__ __forceinline__ void ortho_basis(v3 n, v3& t, v3& b) {
-  v3 up = absx(n.z) < 0.999f ? mk3(0.f, 0.f, 1.f) : mk3(1.f, 0.f, 0.f);
+  v3 up = sel3(absx(n.z) < 0.999f, mk3(0.f, 0.f, 1.f), mk3(1.f, 0.f, 0.f));
   t = safe_normalize(cross3(up, n));
   b = cross3(n, t);
 }
@@ -447,20 +447,51 @@ __device__ __forceinline__ float pdf_ggx(v3 n, v3 v, v3 l, float roughness) {
 // :109-111
 __device__ __forceinline__ float pdf_lambert(v3 n, v3 l) { return fmaxx(dot3(n, l), 0.0f) / PT_PI; }
 
-template <bool STATS, bool TEX>
-__device__ __forceinline__ float trace_shadow_dist(ShadeCtx& c, v3 o, v3 d, float maxd, uint32_t seed, TraversalCounters& cnt) {
-  c.shadow_rays++;
-  Ray r = make_ray(o, d, 0.001f, maxd);
-  return trace_any<STATS, TEX>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
-}
+// NEE visibility, deferred. closest_hit (pt_shade.h) only records the shadow ray and the light's
+// contribution with the visibility factor left out; the ray-gen loop traces the ray once shading is
+// done (resolve_shadow), so no shading state is live across the any-hit traversal (round 1: 164 B
+// per lane of scratch spills in pt_camera_kernel). The result is bit-identical to tracing inside
+// sampleLights / samplePunctualLights (closesthit.rchit:115-126, :180-188, :290-318):
+//   - the shadow ray (origin, direction, range) is built from the same expressions (:119-126);
+//   - the contribution keeps the reference's operation order with vis in place:
+//     lo + ((pre * vis) * post), and for mixed light sets lc = (0 + that) * (1 / p) (:476-488);
+//   - vis = max(vis, transmission) and the `vis > 0` / `pdf_nee > 1e-10` guards are applied as
+//     there, and the any-hit seed is the payload seed of the hit (unchanged until the loop's RR).
+#define SQ_TRACE 1u  // a shadow ray was cast (counted in the shadow-ray statistics)
+#define SQ_VALID 2u  // the light contributes when visible
+#define SQ_MIXED 4u  // emissive + punctual lights: lc = lc * (1 / p_select) before lo += lc
+struct ShadowQuery {
+  v3 o, d;
+  float tmax;
+  v3 pre;       // contribution up to the visibility factor
+  float post;   // factor applied after it (num_lights / ambientLight.w)
+  float scale;  // 1 / p_emissive or 1 / (1 - p_emissive) for SQ_MIXED
+  float trans;  // vis = max(vis, transmission)
+  uint32_t flags;
+};
 
-// :119-126
-template <bool STATS, bool TEX>
-__device__ __forceinline__ float trace_shadow(ShadeCtx& c, v3 o, v3 light_pos, uint32_t seed, TraversalCounters& cnt) {
+// closesthit.rchit:119-126 traceShadow: ray from o towards light_pos, range dist - 0.005
+__device__ __forceinline__ void shadow_towards(ShadowQuery& q, v3 o, v3 light_pos) {
   v3 l = light_pos - o;
   float dist = length3(l);
-  l = safe_normalize(l);
-  return trace_shadow_dist<STATS, TEX>(c, o, l, dist - 0.005f, seed, cnt);
+  q.o = o;
+  q.d = safe_normalize(l);
+  q.tmax = dist - 0.005f;
+}
+
+template <bool STATS, bool TEX>
+__device__ __forceinline__ void resolve_shadow(ShadeCtx& c, v3& color, uint32_t seed, const ShadowQuery& q,
+                                               TraversalCounters& cnt) {
+  if (!(q.flags & SQ_TRACE)) return;
+  c.shadow_rays++;
+  const Ray r = make_ray(q.o, q.d, 0.001f, q.tmax);
+  float vis = trace_any<STATS, TEX>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
+  vis = fmaxx(vis, q.trans);
+  if (vis > 0.0f && (q.flags & SQ_VALID)) {
+    v3 contrib = (q.pre * vis) * q.post;
+    if (q.flags & SQ_MIXED) contrib = (mk3(0.0f) + contrib) * q.scale;
+    color = color + contrib;
+  }
 }
 
 // binary search over a CDF (closesthit.rchit:131-137 / :197-203 / :262-268)
@@ -475,10 +506,9 @@ __device__ __forceinline__ uint32_t cdf_search(const CDF* cdf, uint32_t n, float
   return idx;
 }
 
-// :128-192
-template <bool STATS, bool TEX>
-__device__ void sample_punctual(ShadeCtx& c, const Payload& p, v3 hit_pos, v3 n, v3 n_geo, v3 v, v3 albedo,
-                                float roughness, v3 f0, float transmission, v3& lo, TraversalCounters& cnt) {
+// :128-192 (the shadow ray and the contribution go to q; see ShadowQuery)
+__device__ void sample_punctual(const ShadeCtx& c, const Payload& p, v3 hit_pos, v3 n, v3 n_geo, v3 v, v3 albedo,
+                                float roughness, v3 f0, float transmission, ShadowQuery& q) {
   const DevScene& sc = *c.sc;
   uint32_t num_lights = sc.num_plights;
   float r_select = blue_noise_dim(p, 4);
@@ -515,29 +545,31 @@ __device__ void sample_punctual(ShadeCtx& c, const Payload& p, v3 hit_pos, v3 n,
   if (ndl < 0.001f) return;
   if (ndl > 0.0f && length3(le) > 0.0f) {
     v3 so = hit_pos + n_geo * 0.001f;
-    float vis;
-    if (light.type == 1) vis = trace_shadow_dist<STATS, TEX>(c, so, l, 10000.0f, p.seed, cnt);
-    else vis = trace_shadow<STATS, TEX>(c, so, lpos, p.seed, cnt);
-    vis = fmaxx(vis, transmission);
-    if (vis > 0.0f) {
-      float weight = (float)num_lights;
-      v3 h = safe_normalize(v + l);
-      float ndf = d_ggx(n, h, roughness);
-      float vis_t = v_smith(dot3(n, v), ndl, roughness);
-      v3 f = f_schlick(dot3(h, v), f0);
-      v3 kd = (mk3(1.0f) - f) * (1.0f - transmission);
-      v3 spec = f * (ndf * vis_t);
-      v3 diff = ((kd * albedo) / PT_PI) * (1.0f - transmission);
-      lo = lo + ((((diff + spec) * le) * ndl) * vis) * weight;
+    if (light.type == 1) {  // traceShadowRay with a 1e4 range (:146, :175)
+      q.o = so;
+      q.d = l;
+      q.tmax = 10000.0f;
+    } else {
+      shadow_towards(q, so, lpos);
     }
+    q.trans = transmission;
+    float weight = (float)num_lights;
+    v3 h = safe_normalize(v + l);
+    float ndf = d_ggx(n, h, roughness);
+    float vis_t = v_smith(dot3(n, v), ndl, roughness);
+    v3 f = f_schlick(dot3(h, v), f0);
+    v3 kd = (mk3(1.0f) - f) * (1.0f - transmission);
+    v3 spec = f * (ndf * vis_t);
+    v3 diff = ((kd * albedo) / PT_PI) * (1.0f - transmission);
+    q.pre = ((diff + spec) * le) * ndl;  // lo += ((((diff + spec) * le) * ndl) * vis) * weight
+    q.post = weight;
+    q.flags = SQ_TRACE | SQ_VALID;
   }
 }
 
-// :194-257 (sg == true) and :259-320 (sg == false)
-template <bool STATS, bool TEX>
-__device__ void sample_emissive(ShadeCtx& c, const Payload& p, bool sg, v3 hit_pos, v3 n, v3 n_geo, v3 v,
-                                v3 albedo, float roughness, float metallic, v3 f0, float transmission, v3& lo,
-                                TraversalCounters& cnt) {
+// :194-257 (sg == true) and :259-320 (sg == false); the shadow ray and the contribution go to q
+__device__ void sample_emissive(const ShadeCtx& c, const Payload& p, bool sg, v3 hit_pos, v3 n, v3 n_geo, v3 v,
+                                v3 albedo, float roughness, float metallic, v3 f0, float transmission, ShadowQuery& q) {
   const DevScene& sc = *c.sc;
   uint32_t num = sc.num_light_cdf;
   float r_select = blue_noise_dim(p, sg ? 4 : 7);
@@ -564,40 +596,42 @@ __device__ void sample_emissive(ShadeCtx& c, const Payload& p, bool sg, v3 hit_p
   float ldn = absx(dot3(-l, ln));
   if (ndl > 0.0f && ldn > 0.0f) {
     v3 so = hit_pos + n_geo * 0.001f;
-    float vis = trace_shadow<STATS, TEX>(c, so, lp, p.seed, cnt);
-    vis = fmaxx(vis, transmission);
-    if (vis > 0.0f) {
-      const ptgs_material& lm = sc.materials[light_mat];
-      v3 le = ld3(lm.emissive_factor_and_pad);
-      float es = fmaxx(le.x, fmaxx(le.y, le.z));
-      float pdf_nee = (es / c.cp->emissive_flux) * (dist_sq / ldn);
-      float prob_spec;
-      float pdf_spec, pdf_diff;
-      if (sg) {
-        pdf_spec = pdf_ggx(n, v, l, roughness);
-        pdf_diff = pdf_lambert(n, l);
-        prob_spec = clampf(length3(f0), 0.05f, 0.95f);
-      } else {
-        prob_spec = mixf(0.04f, 1.0f, metallic);
-        pdf_spec = pdf_ggx(n, v, l, roughness);
-        pdf_diff = pdf_lambert(n, l);
-      }
-      float prob_diff = 1.0f - prob_spec;
-      float pdf_bsdf = pdf_spec * prob_spec + pdf_diff * prob_diff;
-      float mis = (pdf_nee * pdf_nee) / (pdf_nee * pdf_nee + pdf_bsdf * pdf_bsdf);
-      v3 h = safe_normalize(v + l);
-      float ndf = d_ggx(n, h, roughness);
-      float vis_t = v_smith(dot3(n, v), ndl, roughness);
-      v3 f = f_schlick(dot3(h, v), f0);
-      v3 kd = mk3(1.0f) - f;
-      v3 spec = f * (ndf * vis_t);
-      v3 diff = ((kd * albedo) / PT_PI) * (1.0f - transmission);
-      v3 brdf = diff + spec;
-      if (pdf_nee > 1e-10f)
-        lo = lo + (((((brdf * le) * ndl) * (1.0f / pdf_nee)) * mis) * vis) * c.cp->ambient[3];
+    shadow_towards(q, so, lp);
+    q.trans = transmission;
+    q.flags = SQ_TRACE;
+    const ptgs_material& lm = sc.materials[light_mat];
+    v3 le = ld3(lm.emissive_factor_and_pad);
+    float es = fmaxx(le.x, fmaxx(le.y, le.z));
+    float pdf_nee = (es / c.cp->emissive_flux) * (dist_sq / ldn);
+    float prob_spec;
+    float pdf_spec, pdf_diff;
+    if (sg) {
+      pdf_spec = pdf_ggx(n, v, l, roughness);
+      pdf_diff = pdf_lambert(n, l);
+      prob_spec = clampf(length3(f0), 0.05f, 0.95f);
+    } else {
+      prob_spec = mixf(0.04f, 1.0f, metallic);
+      pdf_spec = pdf_ggx(n, v, l, roughness);
+      pdf_diff = pdf_lambert(n, l);
+    }
+    float prob_diff = 1.0f - prob_spec;
+    float pdf_bsdf = pdf_spec * prob_spec + pdf_diff * prob_diff;
+    float mis = (pdf_nee * pdf_nee) / (pdf_nee * pdf_nee + pdf_bsdf * pdf_bsdf);
+    v3 h = safe_normalize(v + l);
+    float ndf = d_ggx(n, h, roughness);
+    float vis_t = v_smith(dot3(n, v), ndl, roughness);
+    v3 f = f_schlick(dot3(h, v), f0);
+    v3 kd = mk3(1.0f) - f;
+    v3 spec = f * (ndf * vis_t);
+    v3 diff = ((kd * albedo) / PT_PI) * (1.0f - transmission);
+    v3 brdf = diff + spec;
+    if (pdf_nee > 1e-10f) {
+      // lo += (((((brdf * le) * ndl) * (1 / pdf_nee)) * mis) * vis) * ambientLight.w
+      q.pre = (((brdf * le) * ndl) * (1.0f / pdf_nee)) * mis;
+      q.post = c.cp->ambient[3];
+      q.flags |= SQ_VALID;
     }
   }
 }
-
 
 }  // namespace ptgs

@@ -57,8 +57,9 @@ __device__ __forceinline__ float4 blue_noise_texel(const DevScene& sc, uint32_t 
   return sc.blue_noise[py * sc.bn_size + px];
 }
 
-// 4 waves per SIMD (<= 128 VGPRs): measured +12% over the unconstrained 3-wave build (163 VGPRs)
-// despite ~150 B/lane of spills outside the traversal loop (tools/ab_pt.py, round 1).
+// 4 waves per SIMD (<= 128 VGPRs). With the NEE shadow ray traced after shading (resolve_shadow)
+// the kernel fits without scratch; round 1 held the shading state across the shadow traversal and
+// spilled 164 B per lane.
 #ifndef PTGS_PT_MIN_WAVES
 #define PTGS_PT_MIN_WAVES 4
 #endif
@@ -118,8 +119,11 @@ __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevSc
         ext_rays++;
         Hit h = trace_closest<STATS, TEX>(sc, ray, p.seed, c.stack, tc);
         if (STATS && h.gid != 0xffffffffu) tc.hits++;
+        ShadowQuery q;
+        q.flags = 0;
         if (h.gid == 0xffffffffu) miss<false>(cp, p);
-        else closest_hit<STATS, false, TEX>(c, p, ray, h, tc);
+        else closest_hit<false, TEX>(c, p, ray, h, q);
+        resolve_shadow<STATS, TEX>(c, p.color, p.seed, q, tc);  // NEE visibility after shading
         acc = acc + p.color * thr;
         acc = vmin(acc, 5.0f);
         if (p.hit_flag < 0.0f) break;
@@ -197,8 +201,11 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
     ext_rays++;
     Hit h = trace_closest<STATS, TEX>(sc, ray, p.seed, c.stack, tc);
     if (STATS && h.gid != 0xffffffffu) tc.hits++;
+    ShadowQuery q;
+    q.flags = 0;
     if (h.gid == 0xffffffffu) miss<true>(cp, p);
-    else closest_hit<STATS, true, TEX>(c, p, ray, h, tc);
+    else closest_hit<true, TEX>(c, p, ray, h, q);
+    resolve_shadow<STATS, TEX>(c, p.color, p.seed, q, tc);
 
     v3 fpos = p.hit_pos;
     float fflag = p.hit_flag;
@@ -219,8 +226,11 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
         ext_rays++;
         Hit h2 = trace_closest<STATS, TEX>(sc, r2, p.seed, c.stack, tc);
         if (STATS && h2.gid != 0xffffffffu) tc.hits++;
+        ShadowQuery q2;
+        q2.flags = 0;
         if (h2.gid == 0xffffffffu) miss<true>(cp, p);
-        else closest_hit<STATS, true, TEX>(c, p, r2, h2, tc);
+        else closest_hit<true, TEX>(c, p, r2, h2, q2);
+        resolve_shadow<STATS, TEX>(c, p.color, p.seed, q2, tc);
         acc = acc + p.color * thr;
         acc = vmin(acc, 5.0f);
         if (p.hit_flag < 1.5f) break;

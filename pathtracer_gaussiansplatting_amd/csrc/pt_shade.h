@@ -22,8 +22,10 @@ __device__ __forceinline__ float compute_lod(const CamParams& cp, const DevTextu
   return fmaxx(raw * 0.7f + bias, 0.0f);
 }
 
-template <bool STATS, bool WITH_HITPOS, bool TEX>
-__device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& hit, TraversalCounters& cnt) {
+// The NEE shadow ray is not traced here: it is returned in q (q.flags == 0: none) and traced by the
+// caller after shading (resolve_shadow, pt_device.h), which adds its contribution to p.color.
+template <bool WITH_HITPOS, bool TEX>
+__device__ void closest_hit(const ShadeCtx& c, Payload& p, const Ray& ray, const Hit& hit, ShadowQuery& q) {
   const DevScene& sc = *c.sc;
   const CamParams& cp = *c.cp;
 
@@ -56,7 +58,7 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
   v3 T = t_geo;
   bool tangent_valid = (absx(tw) > 0.001f) && (length3(T) > 0.001f);
   if (!tangent_valid) {
-    v3 up = (absx(N.y) < 0.999f) ? mk3(0.f, 1.f, 0.f) : mk3(1.f, 0.f, 0.f);
+    v3 up = sel3(absx(N.y) < 0.999f, mk3(0.f, 1.f, 0.f), mk3(1.f, 0.f, 0.f));
     T = safe_normalize(cross3(up, N));
   }
   // :358-385 tangent frame + normal map
@@ -169,27 +171,27 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
     }
   }
 
-  // :470-494
+  // :470-494 (with both light kinds: lc = (0 + contribution) * (1 / p_select), lo += lc)
   bool has_emissive = cp.emissive_flux > 0.0f;
   bool has_punctual = cp.punctual_flux > 0.0f;
   bool sg = (float)sg_bits > 0.0f;
   if (has_emissive && has_punctual) {
-    v3 lc = mk3(0.0f);
     float p_punctual = 1.0f - cp.p_emissive;
     if (blue_noise_dim(p, 10) < cp.p_emissive) {
       if (use_nee) {
-        sample_emissive<STATS, TEX>(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, lc, cnt);
-        lc = lc * (1.0f / cp.p_emissive);
+        sample_emissive(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, q);
+        q.scale = 1.0f / cp.p_emissive;
+        q.flags |= SQ_MIXED;
       }
     } else {
-      sample_punctual<STATS, TEX>(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, lc, cnt);
-      lc = lc * (1.0f / p_punctual);
+      sample_punctual(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, q);
+      q.scale = 1.0f / p_punctual;
+      q.flags |= SQ_MIXED;
     }
-    lo = lo + lc;
   } else if (has_emissive && use_nee) {
-    sample_emissive<STATS, TEX>(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, lo, cnt);
+    sample_emissive(c, p, sg, hit_pos, N, n_geo, V, albedo, roughness, metallic, f0, transmission, q);
   } else if (has_punctual) {
-    sample_punctual<STATS, TEX>(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, lo, cnt);
+    sample_punctual(c, p, hit_pos, N, n_geo, V, albedo, roughness, f0, transmission, q);
   }
   p.color = lo;
 
@@ -197,7 +199,7 @@ __device__ void closest_hit(ShadeCtx& c, Payload& p, const Ray& ray, const Hit& 
   if (transmission > 0.0f) {
     p.hit_flag = 2.0f;
     bool entering = dot3(n_geo_orig, V) > 0.0f;
-    v3 n_refr = entering ? n_geo_orig : -n_geo_orig;
+    v3 n_refr = sel3(entering, n_geo_orig, -n_geo_orig);
     p.next_o = hit_pos - n_refr * 0.001f;
     v3 fv = f_schlick(absx(dot3(n_geo_orig, V)), f0);
     float prob_reflect = fmaxx(fmaxx(fv.x, fv.y), fv.z);
