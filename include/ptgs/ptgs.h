@@ -286,6 +286,9 @@ typedef struct ptgs_trace_stats {
 #define PTGS_FLAG_GPU_BVH 4u         /* ptgs_scene_upload builds the BVH on the GPU (LBVH; fast rebuilds,
                                       * slower traversal than the default host SAH build); falls back to
                                       * the host build when the tree exceeds the traversal stack depth */
+#define PTGS_FLAG_SPLAT_PUBLISH 8u   /* ptgs_splat_gaussians also writes the sorted keys / values of every
+                                      * tile (ptgs_splat_get_buffers; parity tests): off in production,
+                                      * the blend needs neither */
 int ptgs_set_flags(ptgs_ctx* ctx, uint32_t flags);
 int ptgs_stats_reset(ptgs_ctx* ctx, void* hip_stream);
 int ptgs_stats_read(ptgs_ctx* ctx, ptgs_trace_stats* out); /* synchronises the context's device */
@@ -323,7 +326,14 @@ typedef struct ptgs_splat_stats {
 /* out_rgba32f (device W*H): rgb = sum c_i a_i T_i + T_final * bg, a = 1 - T_final.
  * Camera = ubo->view / ubo->proj (reference conventions). Tiles 16x16. Rows of tiles
  * [tile_row_begin, tile_row_end) are rendered (full frame: 0, ~0u) — screen-tile sharding of §8e;
- * pixels outside are left untouched. stats may be NULL (reading it synchronises the stream). */
+ * pixels outside are left untouched.
+ * Stream-ordered when stats == NULL: no host synchronisation, so a frame can be captured into and
+ * replayed from a hipGraph. The (Gaussian, tile) pair buffer of the context's workspace starts at
+ * 8 pairs per Gaussian and grows from the pair counts of earlier frames; a frame whose pair count
+ * exceeds it renders incompletely, and the next call grows the buffer (growth frees buffers, which
+ * waits for the device and invalidates graphs captured before it: capture after a frame with stats).
+ * stats != NULL: the call waits for the frame's pair count, re-runs it after growing the buffer when
+ * it did not fit (the frame is always complete) and fills stats. */
 int ptgs_splat_gaussians(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo* ubo,
                          uint32_t width, uint32_t height, const float bg[3],
                          uint32_t tile_row_begin, uint32_t tile_row_end, float* out_rgba32f,
@@ -354,7 +364,8 @@ int ptgs_gaussians_from_points(ptgs_ctx* ctx, const float* xyz, const uint8_t* r
 /* Debug/parity access to the integer intermediates of the most recent ptgs_splat_gaussians call
  * (device buffers owned by the context, valid until the next splat call):
  * radii[N] (int32), tiles_touched[N] (u32), sorted keys[K] (u64: tile<<32 | depth bits),
- * sorted values[K] (u32 gaussian index), tile ranges[tiles] (uint2 start,end). */
+ * sorted values[K] (u32 gaussian index), tile ranges[tiles] (uint2 start,end). sorted_keys /
+ * sorted_values are NULL unless that call ran with PTGS_FLAG_SPLAT_PUBLISH and stats. */
 typedef struct ptgs_splat_buffers {
     const int32_t* radii;
     const uint32_t* tiles_touched;

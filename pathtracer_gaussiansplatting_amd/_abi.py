@@ -21,6 +21,7 @@ ACCUM_SUM = 1
 FLAG_COUNT_TRAVERSAL = 1
 FLAG_TIME_STAGES = 2
 FLAG_GPU_BVH = 4
+FLAG_SPLAT_PUBLISH = 8
 
 # ---------------------------------------------------------------------------------------------
 # numpy dtypes for the array structs (byte-compatible with Helpers/GeneralHeaders.h)

@@ -17,7 +17,7 @@ void splat_workspace_destroy(SplatWorkspace* w);
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
-                           ptgs_splat_stats* stats, bool time_stages, hipStream_t s);
+                           ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s);
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
 void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out);
 hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long** keys);

@@ -55,6 +55,7 @@ struct SplatWorkspace {
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
+  bool last_published = false;  // the last frame published its sorted keys / values and was synchronised
   uint32_t sort_r = 3;        // large-tile radix sort: items per work-item (from the previous frame's largest tile)
   uint32_t sort_grid = 256;   // its workgroups (from the previous frame's large-tile count)
   bool sort_attr = false;     // its dynamic-LDS limit raised
@@ -739,7 +740,7 @@ __device__ __forceinline__ void gs_radix_publish(const uint32_t* sd, uint16_t* s
     for (int j = 0; j < 8; ++j) {
       const uint32_t k = k0 + j * GS_SORT_THREADS;
       if (k < n) {
-        keys_out[k] = tbits | sd[k];
+        if (keys_out) keys_out[k] = tbits | sd[k];  // (keys: only for a published frame)
         vals_out[k] = g[j];
       }
     }
@@ -776,14 +777,15 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
     const uint32_t R = ((n + GS_SORT_THREADS - 1) / GS_SORT_THREADS) | 1u;
     if (R <= rmax) {
       const uint32_t h = gs_radix_tile(s_dep, s_dep + capn, s_slot, s_slot + capn, s_cnt, s_red, segw, n, R);
-      gs_radix_publish(s_dep + h * capn, s_slot + h * capn, segw, n, tbits, keys_out + range.x, vals_out + range.x);
+      gs_radix_publish(s_dep + h * capn, s_slot + h * capn, segw, n, tbits, keys_out ? keys_out + range.x : nullptr,
+                       vals_out + range.x);
     } else if (g_dep && n <= GS_RADIX_MAXN && range.y <= g_cap) {
       // global scratch at the tile's pair offset: [2][g_cap] depths, [2][g_cap] positions
       uint32_t* d0 = g_dep + range.x;
       uint16_t* s0 = g_slot + range.x;
       const uint32_t h = gs_radix_tile(d0, d0 + g_cap, s0, s0 + g_cap, s_cnt, s_red, segw, n, R);
-      gs_radix_publish(h ? d0 + g_cap : d0, h ? s0 + g_cap : s0, segw, n, tbits, keys_out + range.x,
-                       vals_out + range.x);
+      gs_radix_publish(h ? d0 + g_cap : d0, h ? s0 + g_cap : s0, segw, n, tbits,
+                       keys_out ? keys_out + range.x : nullptr, vals_out + range.x);
     } else {  // bitonic network in global memory (a frame whose tiles outgrew the scratch)
       bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
         unsigned long long x = seg[a], y = seg[b];
@@ -791,7 +793,7 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
       });
       for (uint32_t k = tid; k < n; k += GS_SORT_THREADS) {
         const unsigned long long v = seg[k];
-        keys_out[range.x + k] = tbits | (v >> 32);
+        if (keys_out) keys_out[range.x + k] = tbits | (v >> 32);
         vals_out[range.x + k] = (uint32_t)v;
       }
     }
@@ -858,24 +860,24 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   const uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
   const uint32_t tile = tile_y * cam.grid_x + tile_x;
   const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
-  // quadrant mask of a record's alpha box: bit q = (x half q & 1, y half q >> 1). (An exact
-  // ellipse-vs-block refinement was measured slower on C2: 74 vs 71 us.)
-  auto quad_mask = [&](const float4& a, const float4& c) -> uint32_t {
-    const float x0 = a.x - c.y, x1 = a.x + c.y, y0 = a.y - c.z, y1 = a.y + c.z;
-    const bool xl = x0 <= tx0 + 7.0f && x1 >= tx0, xr = x0 <= tx0 + 15.0f && x1 >= tx0 + 8.0f;
-    const bool yt = y0 <= ty0 + 7.0f && y1 >= ty0, yb = y0 <= ty0 + 15.0f && y1 >= ty0 + 8.0f;
-    return (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
-           ((uint32_t)(xr && yb) << 3);
-  };
-  // stage a record as the quadratic in tile-local pixel coordinates (ux, uy):
-  // z = A ux^2 + B ux uy + C uy^2 + D ux + E uy + F (five FMAs per evaluation instead of seven)
-  auto stage_rec = [&](uint32_t slot, const float4& ga, const float4& gb, const float4& gc) {
+  // Stage a record as the quadratic in tile-local pixel coordinates (ux, uy):
+  // z = A ux^2 + B ux uy + C uy^2 + D ux + E uy + F (five FMAs per evaluation instead of seven), and
+  // return the quadrant mask of its alpha box: bit q = (x half q & 1, y half q >> 1), the box tested
+  // in tile-local coordinates against the quadrants' pixel ranges [0, 7] / [8, 15] (immediates: no
+  // register holds a tile bound across the batch loop; the box's 1% + 0.01 px margin covers the
+  // rounding of the local shift). (An exact ellipse-vs-block refinement measured slower on C2.)
+  auto stage_rec = [&](uint32_t slot, const float4& ga, const float4& gb, const float4& gc) -> uint32_t {
     const float gx = ga.x - tx0, gy = ga.y - ty0, A = ga.z, B = ga.w, C = gb.x;
     const float D = -2.0f * A * gx - B * gy, E = -B * gx - 2.0f * C * gy;
     const float F = ((A * gx * gx + B * gx * gy) + C * gy * gy) + gb.y;
     s_stage[slot].a = make_float4(A, B, C, D);
     s_stage[slot].b = make_float4(E, F, gb.z, gb.w);
     s_stage[slot].c = gc;
+    const float x0 = gx - gc.y, x1 = gx + gc.y, y0 = gy - gc.z, y1 = gy + gc.z;
+    const bool xl = x0 <= 7.0f && x1 >= 0.0f, xr = x0 <= 15.0f && x1 >= 8.0f;
+    const bool yt = y0 <= 7.0f && y1 >= 0.0f, yb = y0 <= 15.0f && y1 >= 8.0f;
+    return (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
+           ((uint32_t)(xr && yb) << 3);
   };
   // the tile's slot row is loaded together with its range (no dependent round trip for small tiles)
 #ifdef GS_PROBE_SLOT_N
@@ -934,12 +936,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       }
     if (npad >= 128) __syncthreads();  // the last exchange reads are done before records overwrite them
     if (tid < n) {
-      stage_rec(tid, ra, rb, rc);
-      s_mask[tid] = (uint8_t)quad_mask(ra, rc);
-#ifndef GS_PROBE_NO_PUBLISH
-      keys_out[range.x + tid] = tbits | (key >> 32);
-      vals_out[range.x + tid] = (uint32_t)(key >> 8) & 0xFFFFFFu;
-#endif
+      s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
+      if (keys_out) {  // published frame only (PTGS_FLAG_SPLAT_PUBLISH): the blend needs neither
+        keys_out[range.x + tid] = tbits | (key >> 32);
+        vals_out[range.x + tid] = (uint32_t)(key >> 8) & 0xFFFFFFu;
+      }
       my_slot = (uint32_t)key & 0xFFu;
       s_sslot[tid] = (uint8_t)my_slot;
     }
@@ -965,11 +966,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         if (tid < n) s_key[r0] = k0;
         if (tid + GS_BLOCK < n) s_key[r1] = k1;
         __syncthreads();
-        for (uint32_t k = tid; k < n; k += GS_BLOCK) {
-          const unsigned long long v = s_key[k];
-          keys_out[range.x + k] = tbits | (v >> 32);
-          vals_out[range.x + k] = (uint32_t)v;
-        }
+        if (keys_out)
+          for (uint32_t k = tid; k < n; k += GS_BLOCK) {
+            const unsigned long long v = s_key[k];
+            keys_out[range.x + k] = tbits | (v >> 32);
+            vals_out[range.x + k] = (uint32_t)v;
+          }
       } else {  // beyond GS_MID without the sort kernel (a frame whose tiles outgrew the previous one's)
         bitonic_flip_sort(n, [&](uint32_t a, uint32_t b) {
           unsigned long long x = seg[a], y = seg[b];
@@ -977,7 +979,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         });
         for (uint32_t k = tid; k < n; k += GS_BLOCK) {
           const unsigned long long v = seg[k];
-          keys_out[range.x + k] = tbits | (v >> 32);
+          if (keys_out) keys_out[range.x + k] = tbits | (v >> 32);
           vals_out[range.x + k] = (uint32_t)v;
         }
         __syncthreads();
@@ -1017,8 +1019,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const uint32_t idx = base + tid;
     if (!small) {
       if (idx < n) {
-        stage_rec(tid, ra, rb, rc);
-        s_mask[tid] = (uint8_t)quad_mask(ra, rc);
+        s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
       }
       // next batch: its records (values loaded a batch ago) and the values of the one after
       if (idx + GS_BLOCK < n) {
@@ -1060,6 +1061,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       const uint4 o4 = *reinterpret_cast<const uint4*>(list + j);  // 4 list entries
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
+#ifdef GS_EVAL_SPLIT
+        if (u == 2) __builtin_amdgcn_sched_barrier(0);
+#endif
         const uint32_t o = u == 0 ? o4.x : u == 1 ? o4.y : u == 2 ? o4.z : o4.w;
         const float4 a = *reinterpret_cast<const float4*>(stage + o);
         const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
@@ -1092,7 +1096,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     }
   }
   if (inside) {
-    const size_t pix = (size_t)py * cam.W + px;
+    // the pixel index is recomputed here from a laundered thread id, so that the one computed before
+    // the batch loop is not kept (spilled) across it
+    uint32_t t2 = tid;
+    asm volatile("" : "+v"(t2));
+    const uint32_t px2 = tile_x * GS_BLOCK_X + ((t2 >> 6) & 1u) * 8u + (t2 & 7u);
+    const uint32_t py2 = tile_y * GS_BLOCK_Y + (t2 >> 7) * 8u + ((t2 & 63u) >> 3);
+    const size_t pix = (size_t)py2 * cam.W + px2;
     if (OVER) {
       const float4 u4 = under[pix];
       out[pix] = make_float4(C0 + T * u4.x, C1 + T * u4.y, C2 + T * u4.z, (1.0f - T) + T * u4.w);
@@ -1106,7 +1116,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
-                           ptgs_splat_stats* stats, bool time_stages, hipStream_t s) {
+                           ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s) {
   hipError_t e;
   if (time_stages && !w->ev[0])
     for (hipEvent_t& ev : w->ev)
@@ -1167,28 +1177,39 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   }
   if (!w->k_host) {
     if ((e = hipHostMalloc((void**)&w->k_host, 16, hipHostMallocCoherent | hipHostMallocMapped))) return e;
+    std::memset(w->k_host, 0, 16);
     if ((e = hipHostGetDevicePointer((void**)&w->k_dev, w->k_host, 0))) return e;
   }
 #ifndef GS_K_EVENT_FLAGS
 #define GS_K_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
 #endif
-  // the K event only signals the host: k_host is fine-grained (coherent) memory the GPU writes past
-  // its caches, so the event needs no system-scope cache release (that fence cost a ~6 us bubble
-  // between the scatter and the blend)
+  // the K event only signals the host (stats requested): k_host is fine-grained (coherent) memory the
+  // GPU writes past its caches, so the event needs no system-scope cache release
   if (!w->k_event && (e = hipEventCreateWithFlags(&w->k_event, GS_K_EVENT_FLAGS))) return e;
-  // The pair buffer is sized from the previous frame's K (x1.25, at least 8 pairs per Gaussian) so
-  // that scatter and blend are enqueued before K is known: the host then waits only for the small
-  // K read-back while the GPU runs on; if K did not fit, both kernels did nothing, the buffers grow
-  // and they run again (first frame / growth only).
+  // Pair capacity. The call is stream-ordered: scatter and blend are enqueued against the current
+  // pair buffer and do nothing when the frame's K exceeds it (the device compares). The buffer starts
+  // at 8 pairs per Gaussian and grows from the K that earlier frames' scatters wrote to pinned host
+  // memory (k_host, read here without waiting: a hint); with stats requested the call waits for this
+  // frame's K and re-runs scatter + blend after growing, so that frame is always complete.
   if (w->pairs.bytes < (size_t)n * 64) {
     if ((e = ensure(w->pairs, (size_t)n * 64))) return e;
-    if ((e = ensure(w->keys_out, (size_t)n * 64))) return e;
     if ((e = ensure(w->vals_out, (size_t)n * 32))) return e;
   }
+  if (publish && (e = ensure(w->keys_out, w->pairs.bytes))) return e;
   auto cap_now = [&]() -> uint32_t {
-    size_t c = std::min(std::min(w->pairs.bytes / 8, w->keys_out.bytes / 8), w->vals_out.bytes / 4);
+    size_t c = std::min(w->pairs.bytes / 8, w->vals_out.bytes / 4);
+    if (publish) c = std::min(c, w->keys_out.bytes / 8);
     return (uint32_t)std::min<size_t>(c, 0xFFFFFFFFu);
   };
+  auto grow = [&](uint32_t K) -> hipError_t {  // (hipFree waits for the frames that use the old buffers)
+    hipError_t e2;
+    if ((e2 = ensure(w->pairs, (size_t)K * 8))) return e2;
+    if ((e2 = ensure(w->vals_out, (size_t)K * 4))) return e2;
+    if (publish && (e2 = ensure(w->keys_out, (size_t)K * 8))) return e2;
+    return hipSuccess;
+  };
+  if (w->k_host[0] > cap_now() && (e = grow(w->k_host[0]))) return e;
+  unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
 
   const uint32_t slot_keys = n < (1u << 24) ? 1u : 0u;  // the register sort packs the gaussian in 24 bits
   PreArgs pa;
@@ -1218,7 +1239,6 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = mark(2))) return e;
 
   const uint32_t rows = cam.row_end - cam.row_begin;
-  bool first = true;
   auto enqueue_tail = [&](uint32_t cap) -> hipError_t {
     hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS),
                        2 * band_lds + (size_t)bgrid.groups * 4, s, bgrid, (const ushort4*)w->rect.p,
@@ -1227,8 +1247,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                        (uint2*)w->ranges.p, (unsigned long long*)w->pairs.p, (unsigned long long*)w->tile_slots.p);
     hipError_t e2 = hipGetLastError();
     if (e2) return e2;
-    if (first && (e2 = hipEventRecord(w->k_event, s))) return e2;  // K is on the host after the scatter
-    first = false;
+    if (stats && (e2 = hipEventRecord(w->k_event, s))) return e2;  // K is on the host after the scatter
     if ((e2 = mark(3))) return e2;
     // tiles above GS_MID pairs: sorted by gs_sort_large_kernel when the previous frame had any (else
     // the blend sorts the rare one itself)
@@ -1252,7 +1271,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
       hipLaunchKernelGGL(gs_sort_large_kernel, dim3(w->sort_grid), dim3(GS_SORT_THREADS), gs_radix_lds(w->sort_r), s,
                          (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
                          (const unsigned long long*)w->tile_slots.p, (const uint32_t*)w->large.p,
-                         (const uint32_t*)w->large_ctr.p, (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p,
+                         (const uint32_t*)w->large_ctr.p, keys_out, (uint32_t*)w->vals_out.p,
                          (const uint32_t*)w->total.p, cap, w->sort_r, g_dep, g_slot, g_cap);
       if ((e2 = hipGetLastError())) return e2;
     }
@@ -1263,7 +1282,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
       const dim3 grid(cam.grid_x, rows);
       hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p,
                          (unsigned long long*)w->pairs.p, sort_large ? (uint32_t)GS_MID : 0xFFFFFFFFu,
-                         (unsigned long long*)w->keys_out.p, (uint32_t*)w->vals_out.p, (const float4*)w->rec.p,
+                         keys_out, (uint32_t*)w->vals_out.p, (const float4*)w->rec.p,
                          bg[0], bg[1], bg[2], (const uint32_t*)w->total.p, cap, slot_keys,
                          (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out);
       if ((e2 = hipGetLastError())) return e2;
@@ -1271,30 +1290,30 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     return mark(6);
   };
   if ((e = enqueue_tail(cap_now()))) return e;
-  if ((e = hipEventSynchronize(w->k_event))) return e;
-  const uint32_t K = w->k_host[0];
-  {  // the next frame's large-tile sort: LDS capacity from the largest tile of the previous frame
-     // (k_host[1]; +1/8 headroom), workgroups from this frame's large-tile count (k_host[2])
-    const uint32_t big = w->k_host[1] + w->k_host[1] / 8u;
-    w->sort_r = std::min((uint32_t)GS_RADIX_MAXR, ((big + GS_SORT_THREADS - 1) / GS_SORT_THREADS) | 1u);
-    w->sort_grid = std::max(64u, std::min(4096u, w->k_host[2] + w->k_host[2] / 4u));
-  }
-  if (K > cap_now()) {  // did not fit: grow (hipFree/hipMalloc order after the no-op kernels) and re-run
-    if ((e = ensure(w->pairs, (size_t)K * 8))) return e;
-    if ((e = ensure(w->keys_out, (size_t)K * 8))) return e;
-    if ((e = ensure(w->vals_out, (size_t)K * 4))) return e;
-    if ((e = mark(2))) return e;
-    if ((e = enqueue_tail(cap_now()))) return e;
-  }
-  w->last_n = n;
-  w->last_k = K;
-  w->last_tiles = tiles;
+  uint32_t K = w->k_host[0];  // without stats: the latest K any frame published (a hint)
   if (stats) {
+    if ((e = hipEventSynchronize(w->k_event))) return e;
+    K = w->k_host[0];
+    if (K > cap_now()) {  // did not fit: grow and re-run scatter, sort and blend
+      if ((e = grow(K))) return e;
+      if ((e = mark(2))) return e;
+      if ((e = enqueue_tail(cap_now()))) return e;
+    }
     stats->num_rendered = K;
     stats->tiles_x = cam.grid_x;
     stats->tiles_y = cam.grid_y;
     stats->num_visible = 0;
   }
+  {  // the next frame's large-tile sort: LDS capacity from the largest tile of a recent frame
+     // (k_host[1]; +1/8 headroom), workgroups from its large-tile count (k_host[2]); hints only
+    const uint32_t big = w->k_host[1] + w->k_host[1] / 8u;
+    w->sort_r = std::min((uint32_t)GS_RADIX_MAXR, ((big + GS_SORT_THREADS - 1) / GS_SORT_THREADS) | 1u);
+    w->sort_grid = std::max(64u, std::min(4096u, w->k_host[2] + w->k_host[2] / 4u));
+  }
+  w->last_n = n;
+  w->last_k = K;
+  w->last_tiles = tiles;
+  w->last_published = publish && stats;
   return hipSuccess;
 }
 
@@ -1311,8 +1330,8 @@ hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms) {
 void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out) {
   out->radii = (const int32_t*)w->radii.p;
   out->tiles_touched = (const uint32_t*)w->touched.p;
-  out->sorted_keys = (const uint64_t*)w->keys_out.p;
-  out->sorted_values = (const uint32_t*)w->vals_out.p;
+  out->sorted_keys = w->last_published ? (const uint64_t*)w->keys_out.p : nullptr;
+  out->sorted_values = w->last_published ? (const uint32_t*)w->vals_out.p : nullptr;
   out->tile_ranges = (const uint32_t*)w->ranges.p;
   out->means2d = (const float*)w->means2d.p;
   out->depths = (const float*)w->depths.p;

@@ -46,14 +46,18 @@ def _stream(stream) -> int:
 
 
 class Renderer:
-    def __init__(self, device: int = 0, lib_path: str | None = None):
+    def __init__(self, device: int = 0, lib_path: str | None = None, publish_splat_buffers: bool = False):
+        """publish_splat_buffers: every synchronised splat (want_stats) also publishes its sorted
+        keys / values for splat_buffers() (PTGS_FLAG_SPLAT_PUBLISH, kept across set_flags)."""
         self.lib = _abi.load_library(lib_path)
+        self._publish = _abi.FLAG_SPLAT_PUBLISH if publish_splat_buffers else 0
         h = C.c_void_p()
         rc = self.lib.ptgs_create(int(device), C.byref(h))
         _abi.check(rc, f"ptgs_create(device={device})")
         self._h = h
         self.device = device
         self.scene = None
+        self.set_flags(0)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -152,7 +156,7 @@ class Renderer:
         self._chk(rc, "ptgs_allreduce_radiance")
 
     def set_flags(self, flags: int):
-        self._chk(self.lib.ptgs_set_flags(self._h, flags), "ptgs_set_flags")
+        self._chk(self.lib.ptgs_set_flags(self._h, flags | self._publish), "ptgs_set_flags")
 
     def stats_reset(self, stream=None):
         self._chk(self.lib.ptgs_stats_reset(self._h, _stream(stream)), "ptgs_stats_reset")

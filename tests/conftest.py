@@ -33,6 +33,6 @@ def renderer(native_lib):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from pathtracer_gaussiansplatting_amd import Renderer
-    r = Renderer(0)
+    r = Renderer(0, publish_splat_buffers=True)
     yield r
     r.close()
