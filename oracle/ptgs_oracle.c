@@ -1475,7 +1475,10 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
     if (trow1 > (uint32_t)gy) trow1 = (uint32_t)gy;
     if (trow1 < trow0) trow1 = trow0;
     uint64_t K = 0;
-    for (uint32_t i = 0; i < n; ++i) {
+    /* per-Gaussian preprocess: independent iterations (OpenMP; K is a sum) */
+#pragma omp parallel for schedule(static, 4096) reduction(+ : K)
+    for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+        const uint32_t i = (uint32_t)ii;
         radii[i] = 0;
         touched[i] = 0;
         float m4[4] = {means[3 * i], means[3 * i + 1], means[3 * i + 2], 1.0f}, pv[4], ph[4];
@@ -1537,8 +1540,15 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
         K += touched[i];
     }
     OPair* pairs = (OPair*)malloc(sizeof(OPair) * (K ? K : 1));
-    uint64_t k = 0;
-    for (uint32_t i = 0; i < n; ++i) {
+    /* duplicate with keys: each Gaussian's pairs at the prefix of the counts (the order before the
+     * total-order qsort below does not matter) */
+    uint64_t* first = (uint64_t*)malloc(sizeof(uint64_t) * ((size_t)n + 1));
+    first[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) first[i + 1] = first[i] + (radii[i] > 0 ? touched[i] : 0);
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+        const uint32_t i = (uint32_t)ii;
+        uint64_t k = first[i];
         if (radii[i] <= 0) continue;
         int r = radii[i];
         float ix = means2d[2 * i], iy = means2d[2 * i + 1];
@@ -1554,6 +1564,7 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
                 k++;
             }
     }
+    free(first);
     qsort(pairs, (size_t)K, sizeof(OPair), cmp_pair);
     uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (K ? K : 1));
     uint32_t* vals = (uint32_t*)malloc(sizeof(uint32_t) * (K ? K : 1));
@@ -1566,10 +1577,11 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
         if (j == 0 || (uint32_t)(keys[j - 1] >> 32) != t) ranges[2 * t] = (uint32_t)j;
         if (j == K - 1 || (uint32_t)(keys[j + 1] >> 32) != t) ranges[2 * t + 1] = (uint32_t)(j + 1);
     }
-    /* blend */
-    for (uint32_t ty = trow0; ty < trow1; ++ty)
-        for (uint32_t tx = 0; tx < (uint32_t)gx; ++tx) {
-            uint32_t t = ty * (uint32_t)gx + tx;
+    /* blend: tiles are independent (OpenMP over the tiles of the rendered rows) */
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t tt = (int64_t)trow0 * gx; tt < (int64_t)trow1 * gx; ++tt) {
+        {
+            const uint32_t t = (uint32_t)tt, ty = t / (uint32_t)gx, tx = t % (uint32_t)gx;
             uint32_t s0 = ranges[2 * t], s1 = ranges[2 * t + 1];
             for (uint32_t ly = 0; ly < (uint32_t)BY; ++ly)
                 for (uint32_t lx = 0; lx < (uint32_t)BX; ++lx) {
@@ -1608,6 +1620,7 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
                     }
                 }
         }
+    }
     *keys_out = keys;
     *vals_out = vals;
     return (int)K;
