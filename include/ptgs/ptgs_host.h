@@ -110,6 +110,30 @@ int ptgs_builder_add_punctual_light(ptgs_scene_builder* b, const ptgs_punctual_l
  * PTGS_ERANGE when capacity < count. Any output pointer may be NULL. */
 int ptgs_read_ply(const char* path, float* xyz, float* normals, uint8_t* rgb, uint32_t capacity, uint32_t* count);
 
+/* ----- torus RaySample generators (Vulkan_Engine/sampling.cpp:5-434, Sampling::updateSampling) ----- */
+/* method = index into the reference's sampling_methods array (GeneralHeaders.h:552-560, the Engine's
+ * current_sampling) */
+#define PTGS_SAMPLING_RANDOM 0
+#define PTGS_SAMPLING_UNIFORM 1
+#define PTGS_SAMPLING_STRATIFIED 2
+#define PTGS_SAMPLING_LHS 3
+#define PTGS_SAMPLING_HALTON 4
+#define PTGS_SAMPLING_IMP_COL 5 /* colour-gradient importance over the previous HitData */
+#define PTGS_SAMPLING_IMP_HIT 6 /* hit-ratio importance over the previous HitData */
+/* n RaySamples in the order the reference uploads them (Morton-sorted, sampling.cpp:356-361).
+ * Random / Stratified / LHS / importance draw from std::mt19937(seed) (the reference: seed 13,
+ * sampling.cpp:3). The importance methods bin the previous samples (prev_samples, n_prev) with their
+ * read-back hits (prev_hits, n_prev_hits; binning stops at the shorter) on a grid_resolution² grid
+ * (0 = the reference's 256); with n_prev == 0 they fall back to Halton (sampling.cpp:389-392).
+ * out may alias prev_samples (the reference regenerates its sample vector in place). */
+int ptgs_generate_samples(int method, uint32_t n, const ptgs_ray_sample* prev_samples, uint32_t n_prev,
+                          const ptgs_hitdata* prev_hits, uint32_t n_prev_hits, uint32_t seed, int grid_resolution,
+                          ptgs_ray_sample* out);
+/* Sampling::sortSamples: std::sort by the 15-bit-per-axis Morton code (not stable; libstdc++ order) */
+int ptgs_sort_samples(ptgs_ray_sample* samples, uint32_t n);
+/* morton2D (sampling.cpp:346-354) */
+uint32_t ptgs_morton2d(float u, float v);
+
 /* Engine::loadScene settings (engine.cpp:1190-1255) with the Engine defaults for absent keys */
 typedef struct ptgs_scene_settings {
     float ambient_light[4];      /* default (0, 0, 0, 1) */

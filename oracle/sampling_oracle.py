@@ -281,6 +281,8 @@ def halton(index: int, base: int) -> np.float32:  # sampling.cpp:5-16
 
 def _grid_dims(n: int):  # sampling.cpp:40-41 / :187-188
     cols = int(math.ceil(math.sqrt(float(n))))
+    if cols == 0:  # n == 0: the reference divides 0.f / 0 but never uses rows
+        return 0, 0
     rows = int(math.ceil(f32(n) / f32(cols)))
     return cols, rows
 

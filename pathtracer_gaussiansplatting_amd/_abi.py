@@ -212,6 +212,9 @@ SYMBOLS = {
     "ptgs_builder_last_error": (C.c_char_p, [_P]),
     "ptgs_image_decode_rgba8": (_I, [_P, C.c_size_t, _P, C.c_size_t, C.POINTER(_U), C.POINTER(_U), C.POINTER(_U)]),
     "ptgs_read_ply": (_I, [C.c_char_p, _P, _P, _P, _U, C.POINTER(_U)]),
+    "ptgs_generate_samples": (_I, [_I, _U, _P, _U, _P, _U, _U, _I, _P]),
+    "ptgs_sort_samples": (_I, [_P, _U]),
+    "ptgs_morton2d": (_U, [C.c_float, C.c_float]),
     "ptgs_builder_add_gltf": (_I, [_P, C.c_char_p, _FP, _FP, _FP, _U]),
     "ptgs_builder_add_punctual_light": (_I, [_P, _P]),
     "ptgs_builder_load_scene_json": (_I, [_P, C.c_char_p, C.c_char_p, _U, C.POINTER(SceneSettings)]),

@@ -21,9 +21,9 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libptgs.so")
 
 SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "capture.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp",
-           "pt_kernels.hip", "raster.hip", "splat.hip", "knn.hip", "gltf.cpp", "image_decode.cpp", "ply.cpp"]
+           "pt_kernels.hip", "raster.hip", "splat.hip", "knn.hip", "gltf.cpp", "image_decode.cpp", "ply.cpp", "sampling.cpp"]
 # pure host code (scene ingest): plain g++, no device pass
-HOST_SOURCES = {"gltf.cpp", "image_decode.cpp", "ply.cpp"}
+HOST_SOURCES = {"gltf.cpp", "image_decode.cpp", "ply.cpp", "sampling.cpp"}
 # per-source extra flags. pt_kernels.hip: SimplifyCFG's common-store sinking merges stores to
 # different Payload fields from the branches of closest_hit into one store through a phi of
 # addresses, which SROA cannot split: the payload then stays a private (scratch) object.

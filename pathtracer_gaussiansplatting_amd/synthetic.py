@@ -5,8 +5,8 @@
                       Helpers/stb_image.h:1858-1872 via Vulkan_Engine/image.cpp:10)
   atrium_scene()      C3: "250k-tri Sponza-like" procedural atrium
   gaussians_c2()      C2/C4: synthetic Gaussians in a camera-space box
-  torus_samples()     RaySample (u,v) inputs for the toroidal tracer (random method of
-                      Vulkan_Engine/sampling.cpp, Morton-sorted like every method there)
+  torus_samples()     RaySample (u,v) inputs for the toroidal tracer (the reference's generators,
+                      Vulkan_Engine/sampling.cpp, via ptgs_generate_samples)
 """
 from __future__ import annotations
 
@@ -243,22 +243,8 @@ def gaussians_c2(n: int = 100_000, seed: int = 1) -> dict:
     }
 
 
-def _morton2(u: np.ndarray, v: np.ndarray) -> np.ndarray:
-    def part(x):
-        x = x.astype(np.uint64) & np.uint64(0xFFFF)
-        x = (x | (x << np.uint64(8))) & np.uint64(0x00FF00FF)
-        x = (x | (x << np.uint64(4))) & np.uint64(0x0F0F0F0F)
-        x = (x | (x << np.uint64(2))) & np.uint64(0x33333333)
-        x = (x | (x << np.uint64(1))) & np.uint64(0x55555555)
-        return x
-    return part(u) | (part(v) << np.uint64(1))
-
-
-def torus_samples(n: int, seed: int = 13) -> np.ndarray:
-    rng = np.random.default_rng(seed)
-    uv = rng.uniform(0.0, 1.0, (n, 2)).astype(np.float32)
-    key = _morton2((uv[:, 0] * 65535).astype(np.uint32), (uv[:, 1] * 65535).astype(np.uint32))
-    uv = uv[np.argsort(key, kind="stable")]
-    out = np.zeros(n, RAY_SAMPLE_DTYPE)
-    out["uv"] = uv
-    return out
+def torus_samples(n: int, method: int = 0, seed: int = 13) -> np.ndarray:
+    """The reference's own RaySample generator (default: RANDOM with seed 13, sampling.cpp:164-179),
+    Morton-sorted as the Engine uploads it (product: ptgs_generate_samples)."""
+    from .sampling import update_sampling
+    return update_sampling(method, n, seed=seed)
