@@ -1209,7 +1209,6 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     return hipSuccess;
   };
   if (w->k_host[0] > cap_now() && (e = grow(w->k_host[0]))) return e;
-  unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
 
   const uint32_t slot_keys = n < (1u << 24) ? 1u : 0u;  // the register sort packs the gaussian in 24 bits
   PreArgs pa;
@@ -1240,6 +1239,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
 
   const uint32_t rows = cam.row_end - cam.row_begin;
   auto enqueue_tail = [&](uint32_t cap) -> hipError_t {
+    // (read here, not before: grow() may have moved the published-keys buffer since the last call)
+    unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
     hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS),
                        2 * band_lds + (size_t)bgrid.groups * 4, s, bgrid, (const ushort4*)w->rect.p,
                        (const float*)w->depths.p, n, (const uint32_t*)w->hist.p, (const uint2*)w->tile_info.p,

@@ -243,6 +243,17 @@ def gaussians_c2(n: int = 100_000, seed: int = 1) -> dict:
     }
 
 
+def gaussians_in_view(n: int, seed: int, ubo) -> dict:
+    """gaussians_c2 placed in the world frame of the camera `ubo` (BASELINE C4 / C5: the Gaussians sit
+    in the path-traced mesh's view frustum, some in front of and some behind the mesh)."""
+    g = gaussians_c2(n, seed=seed)
+    view = np.array(ubo.view, np.float64).reshape(4, 4).T  # column-major -> row-major
+    inv = np.linalg.inv(view)
+    m = g["means"].astype(np.float64)
+    g["means"] = (m @ inv[:3, :3].T + inv[:3, 3]).astype(np.float32)
+    return g
+
+
 def torus_samples(n: int, method: int = 0, seed: int = 13) -> np.ndarray:
     """The reference's own RaySample generator (default: RANDOM with seed 13, sampling.cpp:164-179),
     Morton-sorted as the Engine uploads it (product: ptgs_generate_samples)."""

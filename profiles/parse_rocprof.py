@@ -2,27 +2,38 @@
 """Summarise a profiles/profile.sh run (gpurun_out/prof_<tag>/) into committed files:
 
   profiles/<tag>_kernel_stats.csv    rocprofv3 --kernel-trace --stats summary (as produced)
-  profiles/<tag>_summary.md          per-kernel average duration + HBM bytes per dispatch
-  profiles/traffic_latest.json       HBM bytes per launch of pt_camera_kernel (read by bench.py)
+  profiles/<tag>_summary.md          per-kernel duration, HBM bytes, L2 hit rate, VALU utilisation
+  profiles/traffic_latest.json       per-kernel HBM bytes per launch + duration (read by bench.py,
+                                     keyed to the sha256 of the profiled libptgs.so)
 
 HBM bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and
 on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read (MI355X_MICROARCH.md §HBM).
-The instrumented (counting) pt_camera_kernel<true> dispatch is told apart by its VGPR count.
+L2 hit rate = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum).
+VALU lane utilisation = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU) (active lanes per issued
+VALU cycle); VALU issue share = SQ_ACTIVE_INST_VALU / SQ_ACTIVE_INST_ANY; wave wait share =
+SQ_WAIT_ANY / SQ_WAVE_CYCLES.
+Dispatch kinds of one kernel name are told apart by their VGPR count (the instrumented counting
+pt_camera_kernel<true> differs from the timed one).
 """
 import csv
 import glob
+import hashlib
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# kernels bench.py reports a roofline for: short key -> substring of the demangled name
+TRACKED = {"pt_camera_kernel": "pt_camera_kernel<false", "gs_sort_blend_kernel": "gs_sort_blend_kernel<false",
+           "pt_extend_kernel": "pt_extend_kernel", "pt_shade_kernel": "pt_shade_kernel",
+           "pt_shadow_kernel": "pt_shadow_kernel", "pt_raygen_kernel": "pt_raygen_kernel"}
 
 
 def _find(d, pat):
-    hits = glob.glob(os.path.join(d, "**", pat), recursive=True)
-    return sorted(hits)
+    return sorted(glob.glob(os.path.join(d, "**", pat), recursive=True))
 
 
 def _counters(d):
@@ -33,69 +44,91 @@ def _counters(d):
     return rows
 
 
+def _short(name):
+    m = re.search(r"ptgs::(\w+)(<[^>(]*>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name[:60]
+
+
 def main(tag, workload):
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     stats = _find(os.path.join(base, "kt"), "*kernel_stats.csv")
     if not stats:
         raise SystemExit(f"no kernel_stats.csv under {base}/kt")
-    dst = os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv")
-    shutil.copy(stats[0], dst)
+    shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     with open(stats[0]) as fh:
         krows = list(csv.DictReader(fh))
-    traces = _find(os.path.join(base, "kt"), "*kernel_trace.csv")
-    per_vgpr = defaultdict(list)
-    if traces:
-        with open(traces[0]) as fh:
+    per_kind = defaultdict(list)  # (name, vgpr) -> durations (ns)
+    for f in _find(os.path.join(base, "kt"), "*kernel_trace.csv"):
+        with open(f) as fh:
             for r in csv.DictReader(fh):
-                name = r.get("Kernel_Name", "")
-                dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                per_vgpr[(name, r.get("VGPR_Count", "?"))].append(dur)
-    by_kernel = defaultdict(lambda: defaultdict(list))  # (name, vgpr) -> counter -> values
-    for sub in ("fetch", "write"):
+                per_kind[(r.get("Kernel_Name", ""), r.get("VGPR_Count", "?"))].append(
+                    int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    cnt = defaultdict(lambda: defaultdict(list))  # (name, vgpr) -> counter -> per-dispatch values
+    for sub in ("fetch", "write", "tcc", "sq"):
         for r in _counters(os.path.join(base, sub)):
-            key = (r["Kernel_Name"], r.get("VGPR_Count", "?"))
-            by_kernel[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            cnt[(r["Kernel_Name"], r.get("VGPR_Count", "?"))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+
+    def avg(c, k):
+        v = c.get(k, [])
+        return sum(v) / len(v) if v else float("nan")
+
     lines = [f"# rocprofv3 summary — {tag}", "", f"workload: {workload}", "",
              "## kernel-trace --stats (as reported)", "",
              "| kernel | calls | avg ms | total ms | % |", "|---|---|---|---|---|"]
     for r in krows:
         lines.append(f"| {r['Name'][:90]} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.4f} | "
                      f"{float(r['TotalDurationNs']) / 1e6:.3f} | {float(r['Percentage']):.2f} |")
-    lines += ["", "## per dispatch kind (kernel trace, split by VGPR count)", "",
-              "| kernel | VGPRs | dispatches | avg ms |", "|---|---|---|---|"]
-    for (name, vg), durs in sorted(per_vgpr.items(), key=lambda kv: -sum(kv[1])):
-        lines.append(f"| {name[:90]} | {vg} | {len(durs)} | {sum(durs) / len(durs) / 1e6:.4f} |")
-    lines += ["", "## HBM traffic per dispatch (separate --pmc passes)", "",
-              "| kernel | VGPRs | FETCH_SIZE KiB | WRITE_SIZE KiB | HBM bytes (2*F+W)*1024 |", "|---|---|---|---|---|"]
-    traffic = {}
-    for (name, vg), cnt in sorted(by_kernel.items()):
-        f = cnt.get("FETCH_SIZE", [])
-        w = cnt.get("WRITE_SIZE", [])
-        fa = sum(f) / len(f) if f else float("nan")
-        wa = sum(w) / len(w) if w else float("nan")
+    lines += ["", "## per dispatch kind (kernel trace split by VGPR count; counters from separate --pmc passes)", "",
+              "| kernel | VGPRs | dispatches | avg ms | FETCH KiB | WRITE KiB | HBM bytes (2F+W)·1024 | HBM GB/s | "
+              "frac of 8 TB/s | L2 hit | VALU lanes | VALU issue | wave wait |",
+              "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    out = {"tag": tag, "workload": workload,
+           "lib_sha256": hashlib.sha256(open(os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", "libptgs.so"),
+                                             "rb").read()).hexdigest(),
+           "formula": {"hbm_bytes": "(2*FETCH_SIZE + WRITE_SIZE) * 1024", "l2_hit": "TCC_HIT/(TCC_HIT+TCC_MISS)",
+                       "valu_lanes": "SQ_THREAD_CYCLES_VALU/(64*SQ_ACTIVE_INST_VALU)"},
+           "kernels": {}}
+    for (name, vg), durs in sorted(per_kind.items(), key=lambda kv: -sum(kv[1])):
+        c = cnt.get((name, vg), {})
+        ms = sum(durs) / len(durs) / 1e6
+        fa, wa = avg(c, "FETCH_SIZE"), avg(c, "WRITE_SIZE")
         hbm = (2 * fa + wa) * 1024
-        lines.append(f"| {name[:90]} | {vg} | {fa:.1f} | {wa:.1f} | {hbm:.4g} |")
-        if "pt_camera_kernel<false" in name:
-            traffic.setdefault("candidates", []).append({"name": name, "vgpr": vg, "hbm": hbm,
-                                                         "fetch_kib": fa, "write_kib": wa})
-    # the timed (non-instrumented) pt kernel is the <false> instantiation (profile.sh keeps full names)
-    cands = traffic.get("candidates", [])
-    import hashlib
-    lib = os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", "libptgs.so")
-    out = {"tag": tag, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest()}
-    if cands:
-        c = cands[0]
-        out["pt_camera_kernel"] = {"workload": workload, "hbm_bytes_per_launch": c["hbm"], "vgpr": c["vgpr"],
-                                   "fetch_kib": c["fetch_kib"], "write_kib": c["write_kib"],
-                                   "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024"}
+        gbs = hbm / (ms * 1e-3) / 1e9 if ms > 0 else float("nan")
+        hit, miss = avg(c, "TCC_HIT_sum"), avg(c, "TCC_MISS_sum")
+        l2 = _div(hit, hit + miss)
+        lanes = _div(avg(c, "SQ_THREAD_CYCLES_VALU"), 64 * avg(c, "SQ_ACTIVE_INST_VALU"))
+        issue = _div(avg(c, "SQ_ACTIVE_INST_VALU"), avg(c, "SQ_ACTIVE_INST_ANY"))
+        wait = _div(avg(c, "SQ_WAIT_ANY"), avg(c, "SQ_WAVE_CYCLES"))
+        lines.append(f"| {name[:80]} | {vg} | {len(durs)} | {ms:.4f} | {fa:.1f} | {wa:.1f} | {hbm:.4g} | {gbs:.1f} | "
+                     f"{gbs / 8000:.4f} | {l2:.3f} | {lanes:.3f} | {issue:.3f} | {wait:.3f} |")
+        for key, pat in TRACKED.items():
+            if pat in name and key not in out["kernels"]:
+                out["kernels"][key] = {"name": _short(name), "vgpr": vg, "dispatches": len(durs), "avg_ms": ms,
+                                       "fetch_kib": fa, "write_kib": wa, "hbm_bytes_per_launch": hbm,
+                                       "hbm_gbs": gbs, "l2_hit": l2, "valu_lane_util": lanes,
+                                       "valu_issue_share": issue, "wave_wait_share": wait}
     with open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w") as fh:
         fh.write("\n".join(lines) + "\n")
+    out = _finite(out)
     with open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print("\n".join(lines))
     print(json.dumps(out, indent=1))
 
 
+def _div(a, b):
+    return a / b if b else float("nan")
+
+
+def _finite(x):
+    """NaN (a counter pass that did not see the kernel) -> null, so the JSON stays standard."""
+    if isinstance(x, dict):
+        return {k: _finite(v) for k, v in x.items()}
+    if isinstance(x, float) and x != x:
+        return None
+    return x
+
+
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01",
-         sys.argv[2] if len(sys.argv) > 2 else "C3 1920x1080 64spp 250000tri")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r02",
+         sys.argv[2] if len(sys.argv) > 2 else "C3 1920x1080 64spp 250000tri + C2 100000 Gaussians 1920x1080")

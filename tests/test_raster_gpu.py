@@ -119,6 +119,35 @@ def test_gaussians_beyond_24bit_indices(renderer, oracle_lib):
         assert U.rel_l2(out.cpu().numpy(), ref["image"]) < 1e-4
 
 
+def test_gaussians_first_frame_overflow_rerun_published(native_lib, oracle_lib):
+    """A fresh context's first dense frame needs more pairs than the initial buffer (8 per Gaussian, +25%):
+    with stats requested the call grows the buffers and re-runs scatter, sort and blend. The re-run
+    must publish into the grown keys buffer (it once wrote the freed one: a GPU fault at C5's size)."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H = 256, 144
+    g = Y.gaussians_c2(3000, seed=21)
+    g["scales"] *= 16.0  # large radii: K > 10 n, the initial capacity
+    ubo = _gauss_ubo(W, H)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H)
+    assert ref["K"] > 10 * 3000, ref["K"]
+    r = Renderer(0, publish_splat_buffers=True)
+    try:
+        small = {k: _dev(v) for k, v in Y.gaussians_c2(3000, seed=1).items()}
+        r.splat_gaussians(small, ubo, W, H, torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"))
+        dg = {k: _dev(v) for k, v in g.items()}
+        for frame in range(2):  # frame 0: overflow + re-run; frame 1: the grown buffers
+            out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            st = r.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
+            torch.cuda.synchronize()
+            b = r.splat_buffers()
+            assert st.num_rendered == ref["K"]
+            np.testing.assert_array_equal(_read(r, b.sorted_keys, ref["K"], np.uint64), ref["keys"])
+            np.testing.assert_array_equal(_read(r, b.sorted_values, ref["K"], np.uint32), ref["vals"])
+            assert U.rel_l2(out.cpu().numpy(), ref["image"]) < 1e-4, frame
+    finally:
+        r.close()
+
+
 def test_gaussians_stream_ordered_graph_replay(renderer, oracle_lib):
     """Without stats ptgs_splat_gaussians never waits on the host (ptgs.h): a C2-sized frame (100k
     Gaussians, 1920x1080) is captured into a hipGraph and replayed; the replays reproduce the oracle
