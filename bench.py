@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-pt", action="store_true")
     ap.add_argument("--no-hybrid", action="store_true")
     ap.add_argument("--no-gpu-bvh", action="store_true")
+    ap.add_argument("--no-wavefront", action="store_true")
     ap.add_argument("--no-gs-1m", action="store_true", help="skip the 1M-Gaussian splat and the point-cloud init legs")
     ap.add_argument("--no-gs-10m", action="store_true", help="skip the 10M-Gaussian 3840x2160 splat leg (C5's splat)")
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
@@ -236,6 +237,27 @@ def main():
                 "note": "cache-inclusive: B_pt (SURVEY 8d) prices every BVH node / triangle / shading fetch the "
                         "kernel issues; the C3 scene is L2/MALL-resident, so it is priced against the L2 peak"}),
         })
+        # the wavefront path tracer (PTGS_FLAG_PT_WAVEFRONT) on the same frames: raygen / extend / shade /
+        # shadow / accumulate stages over compacted ray queues
+        if not args.no_wavefront:
+            r.set_wavefront(True)
+            for _ in range(max(args.warmup, 1)):
+                pt_step()
+            torch.cuda.synchronize()
+            r.stats_reset(stream)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(args.steps):
+                pt_step()
+            torch.cuda.synchronize()
+            barrier()
+            wdt = max_over_ranks(time.perf_counter() - t0)
+            wst = r.stats()
+            r.set_wavefront(False)
+            out["pt_wavefront"] = {"value": round(sum_over_ranks(float(wst.extension_rays + wst.shadow_rays)) / wdt / 1e6,
+                                                  3), "unit": "Mrays/s", "ms_per_step": round(wdt / args.steps * 1e3, 3),
+                                   "note": "same C3 frames through the wavefront stages (PTGS_FLAG_PT_WAVEFRONT)"}
         # the GPU LBVH builder (PTGS_FLAG_GPU_BVH) on the same scene: build time and one traced frame
         if world == 1 and not args.no_gpu_bvh:
             r.set_flags(FLAG_GPU_BVH)

@@ -289,6 +289,10 @@ typedef struct ptgs_trace_stats {
 #define PTGS_FLAG_SPLAT_PUBLISH 8u   /* ptgs_splat_gaussians also writes the sorted keys / values of every
                                       * tile (ptgs_splat_get_buffers; parity tests): off in production,
                                       * the blend needs neither */
+#define PTGS_FLAG_PT_WAVEFRONT 16u  /* ptgs_trace_camera runs the wavefront path tracer (raygen / extend /
+                                      * shade / shadow / accumulate stages over compacted ray queues)
+                                      * instead of the one-kernel-per-frame path loop; same image, same
+                                      * ray counts */
 int ptgs_set_flags(ptgs_ctx* ctx, uint32_t flags);
 int ptgs_stats_reset(ptgs_ctx* ctx, void* hip_stream);
 int ptgs_stats_read(ptgs_ctx* ctx, ptgs_trace_stats* out); /* synchronises the context's device */

@@ -22,6 +22,7 @@ FLAG_COUNT_TRAVERSAL = 1
 FLAG_TIME_STAGES = 2
 FLAG_GPU_BVH = 4
 FLAG_SPLAT_PUBLISH = 8
+FLAG_PT_WAVEFRONT = 16
 
 # ---------------------------------------------------------------------------------------------
 # numpy dtypes for the array structs (byte-compatible with Helpers/GeneralHeaders.h)

@@ -21,13 +21,14 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libptgs.so")
 
 SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "capture.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp",
-           "pt_kernels.hip", "raster.hip", "splat.hip", "knn.hip", "gltf.cpp", "image_decode.cpp", "ply.cpp", "sampling.cpp"]
+           "pt_kernels.hip", "pt_wavefront.hip", "raster.hip", "splat.hip", "knn.hip", "gltf.cpp", "image_decode.cpp", "ply.cpp", "sampling.cpp"]
 # pure host code (scene ingest): plain g++, no device pass
 HOST_SOURCES = {"gltf.cpp", "image_decode.cpp", "ply.cpp", "sampling.cpp"}
 # per-source extra flags. pt_kernels.hip: SimplifyCFG's common-store sinking merges stores to
 # different Payload fields from the branches of closest_hit into one store through a phi of
 # addresses, which SROA cannot split: the payload then stays a private (scratch) object.
-EXTRA = {"pt_kernels.hip": ["-mllvm", "-simplifycfg-sink-common=false"]}
+EXTRA = {"pt_kernels.hip": ["-mllvm", "-simplifycfg-sink-common=false"],
+         "pt_wavefront.hip": ["-mllvm", "-simplifycfg-sink-common=false"]}
 ARCH = os.environ.get("PTGS_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC]

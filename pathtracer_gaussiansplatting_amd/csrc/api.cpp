@@ -25,6 +25,7 @@
 #include "knn.h"
 #include "hostmath.h"
 #include "pt_launch.h"
+#include "pt_wavefront.h"
 #include "comm.h"
 #include "splat.h"
 #include "textures.h"
@@ -41,6 +42,7 @@ struct ptgs_ctx {
   ptgs_scene_info info{};
   unsigned long long* counters = nullptr;  // 8 x u64
   SplatWorkspace* splat = nullptr;
+  ptgs::WfWorkspace wf;  // wavefront path tracer buffers (PTGS_FLAG_PT_WAVEFRONT)
   void* comm = nullptr;  // RCCL communicator (ptgs_comm_create)
 };
 
@@ -142,6 +144,7 @@ void ptgs_destroy(ptgs_ctx* c) {
   (void)hipSetDevice(c->device);
   free_scene(c);
   if (c->counters) (void)hipFree(c->counters);
+  ptgs::wf_workspace_free(c->wf);
   splat_workspace_destroy(c->splat);
   if (c->comm) (void)comm_destroy(c->comm);
   delete c;
@@ -392,9 +395,16 @@ int ptgs_trace_camera_rows(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_
   CamParams cp;
   int rc = fill_cam(c, ubo, cp);
   if (rc) return rc;
-  hipError_t e = launch_pt_camera(c->dsc, cp, accum, w, h, row_begin, row_end, spp, ubo->frame_count, frame_stride,
-                                  accum_mode, c->counters, (c->flags & PTGS_FLAG_COUNT_TRAVERSAL) != 0,
-                                  (hipStream_t)stream);
+  const bool stats = (c->flags & PTGS_FLAG_COUNT_TRAVERSAL) != 0;
+  hipError_t e;
+  if (c->flags & PTGS_FLAG_PT_WAVEFRONT) {
+    e = ptgs::launch_pt_wavefront(c->wf, c->dsc, cp, accum, w, h, row_begin, row_end, spp, ubo->frame_count,
+                                  frame_stride, accum_mode, c->counters, stats, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(c, PTGS_EHIP, "wavefront path tracer: %s", hipGetErrorString(e));
+    return PTGS_OK;
+  }
+  e = launch_pt_camera(c->dsc, cp, accum, w, h, row_begin, row_end, spp, ubo->frame_count, frame_stride, accum_mode,
+                       c->counters, stats, (hipStream_t)stream);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "pt_camera launch: %s", hipGetErrorString(e));
   return PTGS_OK;
 }

@@ -170,10 +170,19 @@ __device__ __forceinline__ bool anyhit_accept(const DevScene& sc, uint32_t mesh,
   return !(alpha_hash(seed, gid) > alpha);
 }
 
+// Out-of-line any-hit for the textured wavefront extend kernel: inlined into its refill loop, the
+// textured any-hit (indices -> vertices -> texture alpha) was miscompiled at -O3 (transparent
+// candidates decided differently from pt_camera_kernel / the oracle; bit-exact with this call, at
+// -O1, or with trace_closest called per ray). Only candidates on non-opaque triangles pay the call.
+__device__ __noinline__ bool anyhit_accept_call(const DevScene& sc, uint32_t mesh, uint32_t prim, float u, float v,
+                                                uint32_t seed, uint32_t gid) {
+  return anyhit_accept<true>(sc, mesh, prim, u, v, seed, gid);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Traversal
 // ---------------------------------------------------------------------------------------------
-template <bool STATS, bool TEX>
+template <bool STATS, bool TEX, bool AH_CALL = false>
 __device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, int leaf, Hit& h,
                                              uint32_t seed, TraversalCounters& cnt) {
   uint32_t L = (uint32_t)(~leaf);
@@ -196,7 +205,9 @@ __device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, i
     uint32_t gid = f2u(c.w);
     if (t == h.t && gid >= h.gid) continue;
     if (sc.has_transparent && (sc.tri_flags[start + k] & 1u)) {
-      if (!anyhit_accept<TEX>(sc, f2u(a.w), f2u(b.w), u, v, seed, gid)) continue;
+      const bool acc = (AH_CALL && TEX) ? anyhit_accept_call(sc, f2u(a.w), f2u(b.w), u, v, seed, gid)
+                                        : anyhit_accept<TEX>(sc, f2u(a.w), f2u(b.w), u, v, seed, gid);
+      if (!acc) continue;
     }
     h.t = t; h.u = u; h.v = v; h.gid = gid; h.slot = start + k;
   }
@@ -337,6 +348,45 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
     if (sp == 0) return false;
     node = stack[(--sp) * PTGS_BLOCK];
   }
+}
+
+__device__ __forceinline__ v4 matvec(const float* m, v4 v) {
+  // GLSL mat4 * vec4 with columns m[0..3], m[4..7], ...: ((c0*x + c1*y) + c2*z) + c3*w
+  return mk4(((m[0] * v.x + m[4] * v.y) + m[8] * v.z) + m[12] * v.w,
+             ((m[1] * v.x + m[5] * v.y) + m[9] * v.z) + m[13] * v.w,
+             ((m[2] * v.x + m[6] * v.y) + m[10] * v.z) + m[14] * v.w,
+             ((m[3] * v.x + m[7] * v.y) + m[11] * v.z) + m[15] * v.w);
+}
+
+// r2 offset of the blue-noise lookup (raygen_camera.rgen:11-15, :19-23)
+__device__ __forceinline__ float4 blue_noise_texel(const DevScene& sc, uint32_t lx, uint32_t ly, uint32_t frame) {
+  const float a1 = 0.75487766624669276f;
+  const float a2 = 0.56984029099805327f;
+  float rx = fractx((float)frame * a1);
+  float ry = fractx((float)frame * a2);
+  int ox = (int)(rx * (float)sc.bn_size);
+  int oy = (int)(ry * (float)sc.bn_size);
+  int px = ((int)lx + ox) & (sc.bn_size - 1);
+  int py = ((int)ly + oy) & (sc.bn_size - 1);
+  return sc.blue_noise[py * sc.bn_size + px];
+}
+
+// raygen_camera.rgen:19-41: blue-noise jittered camera ray of pixel (x, y) for sample `frame`, and
+// the payload seed (index + frame_count * 719393, :21)
+__device__ __forceinline__ void primary_ray(const DevScene& sc, const CamParams& cp, uint32_t x, uint32_t y,
+                                            uint32_t W, uint32_t H, uint32_t frame, v3& ro, v3& rd, float4& blue,
+                                            uint32_t& seed) {
+  blue = blue_noise_texel(sc, x, y, frame);
+  seed = (y * W + x) + frame * 719393u;
+  const float pcx = (float)x + blue.x, pcy = (float)y + blue.y;
+  const float ux = pcx / (float)W, uy = pcy / (float)H;
+  const float dx = ux * 2.0f - 1.0f, dy = uy * 2.0f - 1.0f;
+  const v4 origin = matvec(cp.inv_view, mk4(0.f, 0.f, 0.f, 1.f));
+  const v4 target = matvec(cp.inv_proj, mk4(dx, dy, 1.f, 1.f));
+  const v3 dirc = normalize3(mk3(target.x, target.y, target.z) / target.w);
+  const v4 direction = matvec(cp.inv_view, mk4(dirc.x, dirc.y, dirc.z, 0.f));
+  ro = mk3(origin.x, origin.y, origin.z);
+  rd = normalize3(mk3(direction.x, direction.y, direction.z));
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -16,14 +16,6 @@
 
 namespace ptgs {
 
-__device__ __forceinline__ v4 matvec(const float* m, v4 v) {
-  // GLSL mat4 * vec4 with columns m[0..3], m[4..7], ...: ((c0*x + c1*y) + c2*z) + c3*w
-  return mk4(((m[0] * v.x + m[4] * v.y) + m[8] * v.z) + m[12] * v.w,
-             ((m[1] * v.x + m[5] * v.y) + m[9] * v.z) + m[13] * v.w,
-             ((m[2] * v.x + m[6] * v.y) + m[10] * v.z) + m[14] * v.w,
-             ((m[3] * v.x + m[7] * v.y) + m[11] * v.z) + m[15] * v.w);
-}
-
 __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
   unsigned long long x = v;
 #pragma unroll
@@ -42,19 +34,6 @@ __device__ __forceinline__ void flush_counters(unsigned long long* counters, uin
     atomicAdd(counters + 2, c);
     if (stats) { atomicAdd(counters + 3, d); atomicAdd(counters + 4, e); atomicAdd(counters + 5, f); }
   }
-}
-
-// r2 offset of the blue-noise lookup (raygen_camera.rgen:11-15, :19-23)
-__device__ __forceinline__ float4 blue_noise_texel(const DevScene& sc, uint32_t lx, uint32_t ly, uint32_t frame) {
-  const float a1 = 0.75487766624669276f;
-  const float a2 = 0.56984029099805327f;
-  float rx = fractx((float)frame * a1);
-  float ry = fractx((float)frame * a2);
-  int ox = (int)(rx * (float)sc.bn_size);
-  int oy = (int)(ry * (float)sc.bn_size);
-  int px = ((int)lx + ox) & (sc.bn_size - 1);
-  int py = ((int)ly + oy) & (sc.bn_size - 1);
-  return sc.blue_noise[py * sc.bn_size + px];
 }
 
 // 4 waves per SIMD (<= 128 VGPRs). With the NEE shadow ray traced after shading (resolve_shadow)
@@ -91,18 +70,10 @@ __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevSc
     }
     for (uint32_t s = 0; s < spp; ++s) {
       const uint32_t frame = frame0 + s * stride;
-      float4 blue = blue_noise_texel(sc, x, y, frame);
-      uint32_t index = y * W + x;
-      uint32_t seed = index + frame * 719393u;
-      float pcx = (float)x + blue.x, pcy = (float)y + blue.y;
-      float ux = pcx / (float)W, uy = pcy / (float)H;
-      float dx = ux * 2.0f - 1.0f, dy = uy * 2.0f - 1.0f;
-      v4 origin = matvec(cp.inv_view, mk4(0.f, 0.f, 0.f, 1.f));
-      v4 target = matvec(cp.inv_proj, mk4(dx, dy, 1.f, 1.f));
-      v3 dirc = normalize3(mk3(target.x, target.y, target.z) / target.w);
-      v4 direction = matvec(cp.inv_view, mk4(dirc.x, dirc.y, dirc.z, 0.f));
-      v3 ro = mk3(origin.x, origin.y, origin.z);
-      v3 rd = normalize3(mk3(direction.x, direction.y, direction.z));
+      v3 ro, rd;
+      float4 blue;
+      uint32_t seed;
+      primary_ray(sc, cp, x, y, W, H, frame, ro, rd, blue, seed);
 
       v3 acc = mk3(0.0f);
       v3 thr = mk3(1.0f);

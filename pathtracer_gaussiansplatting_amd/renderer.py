@@ -46,11 +46,14 @@ def _stream(stream) -> int:
 
 
 class Renderer:
-    def __init__(self, device: int = 0, lib_path: str | None = None, publish_splat_buffers: bool = False):
+    def __init__(self, device: int = 0, lib_path: str | None = None, publish_splat_buffers: bool = False,
+                 wavefront: bool = False):
         """publish_splat_buffers: every synchronised splat (want_stats) also publishes its sorted
-        keys / values for splat_buffers() (PTGS_FLAG_SPLAT_PUBLISH, kept across set_flags)."""
+        keys / values for splat_buffers() (PTGS_FLAG_SPLAT_PUBLISH); wavefront: trace_camera runs the
+        wavefront path tracer (PTGS_FLAG_PT_WAVEFRONT). Both are kept across set_flags."""
         self.lib = _abi.load_library(lib_path)
-        self._publish = _abi.FLAG_SPLAT_PUBLISH if publish_splat_buffers else 0
+        self._publish = (_abi.FLAG_SPLAT_PUBLISH if publish_splat_buffers else 0) | (
+            _abi.FLAG_PT_WAVEFRONT if wavefront else 0)
         h = C.c_void_p()
         rc = self.lib.ptgs_create(int(device), C.byref(h))
         _abi.check(rc, f"ptgs_create(device={device})")
@@ -156,7 +159,13 @@ class Renderer:
         self._chk(rc, "ptgs_allreduce_radiance")
 
     def set_flags(self, flags: int):
+        self._flags = flags
         self._chk(self.lib.ptgs_set_flags(self._h, flags | self._publish), "ptgs_set_flags")
+
+    def set_wavefront(self, on: bool):
+        """Select the path tracer of trace_camera: wavefront stages (True) or the one-kernel path loop."""
+        self._publish = (self._publish & ~_abi.FLAG_PT_WAVEFRONT) | (_abi.FLAG_PT_WAVEFRONT if on else 0)
+        self.set_flags(getattr(self, "_flags", 0))
 
     def stats_reset(self, stream=None):
         self._chk(self.lib.ptgs_stats_reset(self._h, _stream(stream)), "ptgs_stats_reset")

@@ -36,3 +36,11 @@ def renderer(native_lib):
     r = Renderer(0, publish_splat_buffers=True)
     yield r
     r.close()
+
+
+@pytest.fixture(params=["megakernel", "wavefront"])
+def pt(renderer, request):
+    """The renderer with either path tracer selected (both must give the oracle's image)."""
+    renderer.set_wavefront(request.param == "wavefront")
+    yield renderer
+    renderer.set_wavefront(False)

@@ -62,14 +62,14 @@ def _trace_rows_counts(renderer, ubo, W, H, spp, rows):
     return renderer.stats(), acc
 
 
-def test_c3_full_frame_every_32nd_row(renderer, oracle_lib):
+def test_c3_full_frame_every_32nd_row(pt, oracle_lib):
     """C3: 250k-tri atrium, 1920x1080, 64 spp (the bench's frame 0) vs the oracle on every 32nd row."""
     W, H, SPP = 1920, 1080, 64
     sc = U.atrium(250_000)
-    renderer.upload_scene(sc)
+    pt.upload_scene(sc)
     ubo = make_ubo(U.atrium_pose(W / H), sc, 0, ambient=AMBIENT, height=H)
     acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
-    renderer.trace_camera(ubo, W, H, acc, spp=SPP, mode=ACCUM_RUNNING_MEAN)
+    pt.trace_camera(ubo, W, H, acc, spp=SPP, mode=ACCUM_RUNNING_MEAN)
     torch.cuda.synchronize()
     got = acc.cpu().numpy()
     ref = np.zeros((H, W, 4), np.float32)
@@ -80,7 +80,7 @@ def test_c3_full_frame_every_32nd_row(renderer, oracle_lib):
     assert err < 1e-4, (err, nd)
     assert nd == 0, f"{nd} pixels differ (rel L2 {err:.2e})"
     # ray counts over one row band (the product has no row stride: rows 512..543 on both sides)
-    st, _ = _trace_rows_counts(renderer, ubo, W, H, SPP, (512, 544))
+    st, _ = _trace_rows_counts(pt, ubo, W, H, SPP, (512, 544))
     ref2 = np.zeros((H, W, 4), np.float32)
     ost2 = oracle_lib.trace_camera(sc.desc(), ubo, W, H, ref2, spp=SPP, rows=(512, 544), row_stride=1)
     assert (st.extension_rays, st.shadow_rays) == (ost2.extension_rays, ost2.shadow_rays)

@@ -16,6 +16,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
+
 def _gpu_render(renderer, scene, ubo, W, H, spp, frame_stride=1, mode=ACCUM_RUNNING_MEAN, rows=None, init=None):
     renderer.upload_scene(scene)
     acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
@@ -44,11 +45,11 @@ def _compare(gpu, ref, st_g, st_o, tol=TOL):
     return err, ndiff
 
 
-def test_cornell_256_1spp(renderer, oracle_lib):
+def test_cornell_256_1spp(pt, oracle_lib):
     """C1: Cornell box (rt-box of bunny_box.json), 256x256, 1 spp, frame 0."""
     sc = U.cornell()
     ubo = make_ubo(U.cornell_pose(), sc, 0)
-    g, sg = _gpu_render(renderer, sc, ubo, 256, 256, 1)
+    g, sg = _gpu_render(pt, sc, ubo, 256, 256, 1)
     o, so = _oracle_render(oracle_lib, sc, ubo, 256, 256, 1)
     err, nd = _compare(g, o, sg, so)
     assert sg.samples == 256 * 256
@@ -56,29 +57,29 @@ def test_cornell_256_1spp(renderer, oracle_lib):
     print(f"cornell rel L2 {err:.2e}, {nd} pixels differ, ext {sg.extension_rays} shadow {sg.shadow_rays}")
 
 
-def test_cornell_running_mean(renderer, oracle_lib):
+def test_cornell_running_mean(pt, oracle_lib):
     """frames 3..6 on top of an existing accumulator (mix(prev, cur, 1/(n+1)), raygen_camera.rgen:80-87)."""
     sc = U.cornell()
     rng = np.random.default_rng(0)
     init = rng.uniform(0, 1, (64, 96, 4)).astype(np.float32)
     ubo = make_ubo(U.cornell_pose(96 / 64), sc, 3)
-    g, sg = _gpu_render(renderer, sc, ubo, 96, 64, 4, init=init)
+    g, sg = _gpu_render(pt, sc, ubo, 96, 64, 4, init=init)
     o, so = _oracle_render(oracle_lib, sc, ubo, 96, 64, 4, init=init)
     _compare(g, o, sg, so)
 
 
-def test_features_all_branches(renderer, oracle_lib):
+def test_features_all_branches(pt, oracle_lib):
     """glass, clearcoat, metal, spec-gloss, emissive object, BLEND/MASK any-hit, point/spot/sun."""
     sc = U.features()
     ubo = make_ubo(U.cornell_pose(160 / 120), sc, 0, ambient=(0.05, 0.05, 0.08, 1.0))
-    g, sg = _gpu_render(renderer, sc, ubo, 160, 120, 3)
+    g, sg = _gpu_render(pt, sc, ubo, 160, 120, 3)
     o, so = _oracle_render(oracle_lib, sc, ubo, 160, 120, 3)
     err, nd = _compare(g, o, sg, so)
     print(f"features rel L2 {err:.2e}, {nd} pixels differ")
 
 
 @pytest.mark.parametrize("use_lod", [0.0, 1.0])
-def test_features_textured(renderer, oracle_lib, use_lod):
+def test_features_textured(pt, oracle_lib, use_lod):
     """closesthit.rchit texture paths: base colour / spec-gloss / metal-rough / clearcoat (+ roughness) /
     emissive (uv_emissive) samples, tangent-space normal map (uv_normal, lod_factor, computeLOD with
     use_lod), texture alpha in any-hit, odd mip chains, repeat wrapping."""
@@ -86,7 +87,7 @@ def test_features_textured(renderer, oracle_lib, use_lod):
     ubo = make_ubo(U.cornell_pose(160 / 120), sc, 0, ambient=(0.05, 0.05, 0.08, 1.0))
     ubo.use_lod = use_lod
     ubo.lod_factor = 0.8
-    g, sg = _gpu_render(renderer, sc, ubo, 160, 120, 3)
+    g, sg = _gpu_render(pt, sc, ubo, 160, 120, 3)
     o, so = _oracle_render(oracle_lib, sc, ubo, 160, 120, 3)
     err, nd = _compare(g, o, sg, so)
     print(f"textured (use_lod {use_lod}) rel L2 {err:.2e}, {nd} pixels differ")
@@ -96,30 +97,30 @@ def test_features_textured(renderer, oracle_lib, use_lod):
     assert U.rel_l2(o, o2) > 1e-2  # the textures change the image
 
 
-def test_atrium_250k(renderer, oracle_lib):
+def test_atrium_250k(pt, oracle_lib):
     """C3 scene (250k triangles, sun + emissive panel) at a reduced resolution."""
     sc = U.atrium()
     ubo = make_ubo(U.atrium_pose(), sc, 0, ambient=(0.3, 0.4, 0.5, 1.0))
-    g, sg = _gpu_render(renderer, sc, ubo, 160, 90, 2)
+    g, sg = _gpu_render(pt, sc, ubo, 160, 90, 2)
     o, so = _oracle_render(oracle_lib, sc, ubo, 160, 90, 2)
     err, nd = _compare(g, o, sg, so)
     print(f"atrium rel L2 {err:.2e}, {nd} pixels differ")
 
 
-def test_sample_shard_sum_mode(renderer, oracle_lib):
+def test_sample_shard_sum_mode(pt, oracle_lib):
     """§8e sample-index shard: rank g of G renders frames g, g+G, ... in SUM mode."""
     sc = U.cornell()
     ubo = make_ubo(U.cornell_pose(), sc, 1)
-    g, sg = _gpu_render(renderer, sc, ubo, 64, 64, 3, frame_stride=4, mode=ACCUM_SUM)
+    g, sg = _gpu_render(pt, sc, ubo, 64, 64, 3, frame_stride=4, mode=ACCUM_SUM)
     o, so = _oracle_render(oracle_lib, sc, ubo, 64, 64, 3, frame_stride=4, mode=ACCUM_SUM)
     _compare(g, o, sg, so)
     assert np.all(g[..., 3] == 3.0)
 
 
-def test_row_range(renderer, oracle_lib):
+def test_row_range(pt, oracle_lib):
     sc = U.cornell()
     ubo = make_ubo(U.cornell_pose(), sc, 0)
-    g, sg = _gpu_render(renderer, sc, ubo, 64, 64, 1, rows=(10, 37))
+    g, sg = _gpu_render(pt, sc, ubo, 64, 64, 1, rows=(10, 37))
     o, so = _oracle_render(oracle_lib, sc, ubo, 64, 64, 1, rows=(10, 37))
     _compare(g, o, sg, so)
     assert np.all(g[:10] == 0) and np.all(g[37:] == 0)
@@ -163,7 +164,7 @@ def test_gpu_bvh_builder_same_image(renderer, scene):
           f"GPU LBVH {info_g.build_ms:.2f} ms ({info_g.num_bvh_nodes} nodes, depth {info_g.bvh_depth})")
 
 
-def test_ingested_scene_json(renderer, oracle_lib):
+def test_ingested_scene_json(pt, oracle_lib):
     """§8f #3: the scene-JSON fixture (three glTF models incl. .glb, skin, lights, every material
     extension and texture format, rt-box, sun) loaded by ptgs_builder_load_scene_json, then path
     traced on the GPU vs the oracle on the same flattened scene (textures and settings included)."""
@@ -181,7 +182,7 @@ def test_ingested_scene_json(renderer, oracle_lib):
     pose = Camera(aspect=W / H).look_at([0.0, 0.2, 4.3], [0.2, -1.2, 0.0])
     ubo = make_ubo(pose, sc, 0, ambient=tuple(st.ambient_light), height=H, use_lod=st.use_lod,
                    lod_factor=st.lod_factor)
-    g, sg = _gpu_render(renderer, sc, ubo, W, H, 4)
+    g, sg = _gpu_render(pt, sc, ubo, W, H, 4)
     o, so = _oracle_render(oracle_lib, sc, ubo, W, H, 4)
     err, nd = _compare(g, o, sg, so)
     print(f"ingested scene rel L2 {err:.2e}, {nd} pixels differ")
