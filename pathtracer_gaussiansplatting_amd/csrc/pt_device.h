@@ -71,11 +71,13 @@ struct TraversalCounters {
 
 // Traversal stack: PTGS_STACK entries per work-item in LDS, interleaved across the 256 work-items
 // of a workgroup (entry k of lane t at [k * 256 + t]: conflict-free ds_read/ds_write_b32).
-// 40 x 256 x 4 B = 40 KiB per workgroup (4 workgroups = 16 waves per CU fill the 160 KiB LDS). A
-// 4-wide node pushes up to 3 entries: the collapse (api.cpp) caps the fan-out until the tree's
-// worst-case stack need fits (4-wide, else 3-, else 2-wide, which the builder's depth bound fits).
+// 39 x 256 x 4 B = 39 KiB per workgroup (+ 1 KiB of slot rings in the wavefront kernels: 4
+// workgroups = 16 waves per CU fill the 160 KiB LDS). A 4-wide node pushes up to 3 entries: the
+// collapse (api.cpp) caps the fan-out until the tree's worst-case stack need fits (4-wide, else 3-,
+// else 2-wide, which the builder's depth bound fits). Needs measured: C3's 250k-triangle atrium 34,
+// C5's 1M-triangle atrium 38.
 #ifndef PTGS_STACK
-#define PTGS_STACK 40
+#define PTGS_STACK 39
 #endif
 #define PTGS_BLOCK 256
 

@@ -7,13 +7,19 @@
 
 #include "pt_device.h"
 
-// rays per wave in the persistent extend / shadow kernels (each wave walks its own run of the queue,
-// refilling finished lanes); shade-kernel workgroups (grid-stride over the queue)
-#ifndef PTGS_WF_RAYS_PER_WAVE
-#define PTGS_WF_RAYS_PER_WAVE 256u
+// slots per wave: the run of pixel slots each wave of the extend / shadow kernels (persistent,
+// refilling finished lanes) and of the shade kernel walks
+#ifndef PTGS_WF_TRACE_RUN
+#define PTGS_WF_TRACE_RUN 256u
 #endif
-#ifndef PTGS_WF_SHADE_BLOCKS
-#define PTGS_WF_SHADE_BLOCKS 4096u
+#ifndef PTGS_WF_BATCH
+#define PTGS_WF_BATCH 8u  // samples per batch (a tile's samples in adjacent waves)
+#endif
+#ifndef PTGS_WF_REFILL
+#define PTGS_WF_REFILL 16u  // idle lanes of a traversal wave that trigger a refill from its run
+#endif
+#ifndef PTGS_WF_SHADE_RUN
+#define PTGS_WF_SHADE_RUN 256u
 #endif
 
 namespace ptgs {
@@ -21,24 +27,27 @@ namespace ptgs {
 struct WfArgs {
   uint32_t W, H, row0, row1;
   uint32_t tiles_x;  // 8x8 pixel tiles per row
-  uint32_t slots;    // pixel slots of the row range (whole tiles)
-  float4* st_thr;    // (throughput, last_pdf)
-  float4* st_w;      // (payload weight, hit_flag)
-  float4* st_acc;    // (acc, max_depth)
+  uint32_t slots;    // slots of the batch: whole 8x8 tiles x batch samples
+  uint32_t batch;    // samples per batch
+  uint32_t frame0;   // frame count of the batch's first sample
+  uint32_t stride;   // frame count step between samples
+  float4 *ray_o, *ray_d;          // (origin, seed) (direction, -) of the pending extension ray
+  float4* hits;                   // (t, u, v, gid)
+  float4 *sh_o, *sh_d, *sh_acc;   // shadow ray: (origin, tmax) (direction, seed) (acc if unoccluded, -)
+  float4* st_thr;                 // (throughput, last_pdf)
+  float4* st_w;                   // (payload weight, hit_flag)
+  float4* st_acc;                 // (acc, max_depth)
+  uint8_t* flags;                 // bit 0 extension ray pending, bit 1 shadow ray pending
+  uint32_t* part;                 // per-workgroup partial ray / sample counts [counter][block]
+  uint32_t part_stride;
 };
 
 // device buffers, grown on demand and reused across calls
 struct WfWorkspace {
-  void* q[2] = {nullptr, nullptr};
-  size_t q_bytes[2] = {0, 0};
-  void* hits = nullptr;
-  size_t hits_bytes = 0;
-  void* sh = nullptr;
-  size_t sh_bytes = 0;
-  void* st = nullptr;
-  size_t st_bytes = 0;
-  void* cnt = nullptr;
-  size_t cnt_bytes = 0;
+  void* slots = nullptr;
+  size_t slots_bytes = 0;
+  void* part = nullptr;
+  size_t part_bytes = 0;
 };
 
 void wf_workspace_free(WfWorkspace& w);
