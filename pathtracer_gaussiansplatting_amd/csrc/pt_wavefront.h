@@ -13,7 +13,7 @@
 #define PTGS_WF_TRACE_RUN 256u
 #endif
 #ifndef PTGS_WF_BATCH
-#define PTGS_WF_BATCH 8u  // samples per batch (a tile's samples in adjacent waves)
+#define PTGS_WF_BATCH 16u  // samples per batch (a tile's samples in adjacent waves)
 #endif
 #ifndef PTGS_WF_REFILL
 #define PTGS_WF_REFILL 16u  // idle lanes of a traversal wave that trigger a refill from its run
@@ -40,6 +40,7 @@ struct WfArgs {
   uint8_t* flags;                 // bit 0 extension ray pending, bit 1 shadow ray pending
   uint32_t* part;                 // per-workgroup partial ray / sample counts [counter][block]
   uint32_t part_stride;
+  uint32_t* live;                 // [2 d] extension rays pending at depth d, [2 d + 1] shadow rays
 };
 
 // device buffers, grown on demand and reused across calls

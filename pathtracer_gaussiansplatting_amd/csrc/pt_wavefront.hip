@@ -65,6 +65,18 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
 
+// Path state streams through HBM once per bounce (GBs per batch): non-temporal loads / stores keep
+// it from evicting the BVH and triangles (17 MB for C3) from L2 / Infinity Cache.
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldnt(const float4* p) {
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void stnt(float4* p, float4 v) {
+  f4v x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(p));
+}
+
 // slot -> (pixel, sample): slot = (tile * batch + s) * 64 + lane over 8x8 pixel tiles in row-major
 // tile order; a wave holds one tile for one sample, and the batch's samples of a tile are adjacent
 // (the megakernel's per-pixel sample loop reuses the same BVH nodes from cache; so do these waves)
@@ -137,14 +149,15 @@ __global__ __launch_bounds__(256) void pt_wf_raygen_kernel(DevScene sc, CamParam
     float4 blue;
     uint32_t seed;
     primary_ray(sc, cp, x, y, a.W, a.H, frame, ro, rd, blue, seed);
-    a.ray_o[slot] = make_float4(ro.x, ro.y, ro.z, u2f(seed));
-    a.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, 0.0f);
+    stnt(a.ray_o + slot, make_float4(ro.x, ro.y, ro.z, u2f(seed)));
+    stnt(a.ray_d + slot, make_float4(rd.x, rd.y, rd.z, 0.0f));
     // throughput 1, last_pdf 0 | weight 1, hit_flag 0 | acc 0, max_depth 12 (:43-48)
-    a.st_thr[slot] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-    a.st_w[slot] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-    a.st_acc[slot] = make_float4(0.0f, 0.0f, 0.0f, (float)WF_MAX_DEPTH);
+    stnt(a.st_thr + slot, make_float4(1.0f, 1.0f, 1.0f, 0.0f));
+    stnt(a.st_w + slot, make_float4(1.0f, 1.0f, 1.0f, 0.0f));
+    stnt(a.st_acc + slot, make_float4(0.0f, 0.0f, 0.0f, (float)WF_MAX_DEPTH));
   }
   if (slot < a.slots) a.flags[slot] = valid ? WF_EXT : 0u;
+  if (blockIdx.x == 0 && threadIdx.x < 2u * (WF_MAX_DEPTH + 1u)) a.live[threadIdx.x] = threadIdx.x == 0 ? 1u : 0u;
   block_count(a.part, a.part_stride, 2, valid ? 1u : 0u, s_red);  // samples
 }
 
@@ -152,7 +165,9 @@ __global__ __launch_bounds__(256) void pt_wf_raygen_kernel(DevScene sc, CamParam
 // extend: closest hit of the pending extension rays (raygen_camera.rgen:51, pt_device.h trace_closest)
 // ------------------------------------------------------------------------------------------------
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(256, 4) void pt_wf_extend_kernel(DevScene sc, WfArgs a, uint32_t per_wave, uint32_t refill) {
+__global__ __launch_bounds__(256, 4) void pt_wf_extend_kernel(DevScene sc, WfArgs a, uint32_t depth, uint32_t per_wave,
+                                                              uint32_t refill) {
+  if (a.live[2u * depth] == 0u) return;  // no path reached this bounce (adaptive depth / RR ended them)
   __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
   __shared__ uint16_t s_ring[4][WF_RING];
   uint32_t* s_red = reinterpret_cast<uint32_t*>(s_ring);  // after the loop: the count reduction
@@ -179,7 +194,7 @@ __global__ __launch_bounds__(256, 4) void pt_wf_extend_kernel(DevScene sc, WfArg
       const uint32_t avail = ss.tail - ss.head, rk = mbcnt64(idle);
       if (!active && rk < avail) {
         slot = ss.at(ss.head + rk);
-        const float4 ro = a.ray_o[slot], rd = a.ray_d[slot];
+        const float4 ro = ldnt(a.ray_o + slot), rd = ldnt(a.ray_d + slot);
         r = make_ray(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), 0.001f, 10000.0f);
         seed = f2u(ro.w);
         h.t = r.tmax; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu;
@@ -219,7 +234,7 @@ __global__ __launch_bounds__(256, 4) void pt_wf_extend_kernel(DevScene sc, WfArg
       node = pop();
     }
     if (node == WF_DONE) {
-      a.hits[slot] = make_float4(h.t, h.u, h.v, u2f(h.gid));
+      stnt(a.hits + slot, make_float4(h.t, h.u, h.v, u2f(h.gid)));
       if (STATS && h.gid != 0xffffffffu) tc.hits++;
       traced++;
       active = false;
@@ -237,11 +252,11 @@ __global__ __launch_bounds__(256, 4) void pt_wf_extend_kernel(DevScene sc, WfArg
 // shade: miss / closest hit + the bounce bookkeeping of raygen_camera.rgen:53-78 for depth `depth`
 // ------------------------------------------------------------------------------------------------
 template <bool TEX>
-__device__ __forceinline__ void wf_shade_slot(const DevScene& sc, const CamParams& cp, const WfArgs& a,
-                                              uint32_t depth, uint32_t slot) {
+__device__ __forceinline__ uint32_t wf_shade_slot(const DevScene& sc, const CamParams& cp, const WfArgs& a,
+                                                  uint32_t depth, uint32_t slot) {
   ShadeCtx c; c.sc = &sc; c.cp = &cp; c.stack = nullptr; c.shadow_rays = 0;
-  const float4 r_o = a.ray_o[slot], r_d = a.ray_d[slot], hv = a.hits[slot];
-  const float4 s_thr = a.st_thr[slot], s_w = a.st_w[slot], s_acc = a.st_acc[slot];
+  const float4 r_o = ldnt(a.ray_o + slot), r_d = ldnt(a.ray_d + slot), hv = ldnt(a.hits + slot);
+  const float4 s_thr = ldnt(a.st_thr + slot), s_w = ldnt(a.st_w + slot), s_acc = ldnt(a.st_acc + slot);
   uint32_t x, y, frame;
   slot_pixel(a, slot, x, y, frame);
   const float4 blue = blue_noise_texel(sc, x, y, frame);
@@ -284,9 +299,9 @@ __device__ __forceinline__ void wf_shade_slot(const DevScene& sc, const CamParam
     }
     const v3 acc_vis = vmin(acc + col_vis * thr, 5.0f);
     // the any-hit seed is the bounce's seed: before this bounce's RR draw
-    a.sh_o[slot] = make_float4(sq.o.x, sq.o.y, sq.o.z, sq.tmax);
-    a.sh_d[slot] = make_float4(sq.d.x, sq.d.y, sq.d.z, u2f(p.seed));
-    a.sh_acc[slot] = make_float4(acc_vis.x, acc_vis.y, acc_vis.z, 0.0f);
+    stnt(a.sh_o + slot, make_float4(sq.o.x, sq.o.y, sq.o.z, sq.tmax));
+    stnt(a.sh_d + slot, make_float4(sq.d.x, sq.d.y, sq.d.z, u2f(p.seed)));
+    stnt(a.sh_acc + slot, make_float4(acc_vis.x, acc_vis.y, acc_vis.z, 0.0f));
   }
   acc = vmin(acc + col_occ * thr, 5.0f);
   // :60-78
@@ -304,23 +319,30 @@ __device__ __forceinline__ void wf_shade_slot(const DevScene& sc, const CamParam
     }
     if (alive && (float)(depth + 1u) >= max_depth) alive = false;
   }
-  a.st_acc[slot] = make_float4(acc.x, acc.y, acc.z, max_depth);
+  stnt(a.st_acc + slot, make_float4(acc.x, acc.y, acc.z, max_depth));
   if (alive) {
-    a.st_thr[slot] = make_float4(thr.x, thr.y, thr.z, p.last_pdf);
-    a.st_w[slot] = make_float4(p.weight.x, p.weight.y, p.weight.z, p.hit_flag);
-    a.ray_o[slot] = make_float4(p.next_o.x, p.next_o.y, p.next_o.z, u2f(p.seed));
-    a.ray_d[slot] = make_float4(p.next_d.x, p.next_d.y, p.next_d.z, 0.0f);
+    stnt(a.st_thr + slot, make_float4(thr.x, thr.y, thr.z, p.last_pdf));
+    stnt(a.st_w + slot, make_float4(p.weight.x, p.weight.y, p.weight.z, p.hit_flag));
+    stnt(a.ray_o + slot, make_float4(p.next_o.x, p.next_o.y, p.next_o.z, u2f(p.seed)));
+    stnt(a.ray_d + slot, make_float4(p.next_d.x, p.next_d.y, p.next_d.z, 0.0f));
   }
-  a.flags[slot] = (uint8_t)((alive ? WF_EXT : 0u) | (traced ? WF_SHADOW : 0u));
+  const uint32_t fl = (alive ? WF_EXT : 0u) | (traced ? WF_SHADOW : 0u);
+  a.flags[slot] = (uint8_t)fl;
+  return fl;
 }
 
 template <bool TEX>
 __global__ __launch_bounds__(256) void pt_wf_shade_kernel(DevScene sc, CamParams cp, WfArgs a, uint32_t depth,
                                                           uint32_t per_wave) {
+  if (a.live[2u * depth] == 0u) return;
   __shared__ uint16_t s_ring[4][WF_RING];
+  __shared__ uint32_t s_any;
+  if (threadIdx.x == 0) s_any = 0u;
+  __syncthreads();
   const uint32_t begin = (blockIdx.x * 4u + (threadIdx.x >> 6)) * per_wave;
   SlotStream ss;
   ss_init(ss, s_ring[threadIdx.x >> 6], begin, min(a.slots, begin + per_wave));
+  uint32_t any = 0;
   for (;;) {  // full waves of live slots
     ss_fill(ss, a.flags, WF_EXT, 64u);
     const uint32_t take = min(64u, ss.tail - ss.head);
@@ -328,7 +350,14 @@ __global__ __launch_bounds__(256) void pt_wf_shade_kernel(DevScene sc, CamParams
     const bool ok = lane_id() < take;
     const uint32_t slot = ok ? ss.at(ss.head + lane_id()) : 0u;
     ss.head += take;
-    if (ok) wf_shade_slot<TEX>(sc, cp, a, depth, slot);
+    if (ok) any |= wf_shade_slot<TEX>(sc, cp, a, depth, slot);
+  }
+  // which stages the next launches have work for (one word each, written once per workgroup)
+  if (any) atomicOr(&s_any, any);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_any & WF_EXT) a.live[2u * (depth + 1u)] = 1u;
+    if (s_any & WF_SHADOW) a.live[2u * depth + 1u] = 1u;
   }
 }
 
@@ -336,7 +365,9 @@ __global__ __launch_bounds__(256) void pt_wf_shade_kernel(DevScene sc, CamParams
 // shadow: any-hit of the pending NEE rays (pt_device.h trace_any); unoccluded -> the "visible" acc
 // ------------------------------------------------------------------------------------------------
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArgs a, uint32_t per_wave, uint32_t refill) {
+__global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArgs a, uint32_t depth, uint32_t per_wave,
+                                                              uint32_t refill) {
+  if (a.live[2u * depth + 1u] == 0u) return;  // no shadow ray at this bounce
   __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
   __shared__ uint16_t s_ring[4][WF_RING];
   uint32_t* s_red = reinterpret_cast<uint32_t*>(s_ring);  // after the loop: the count reduction
@@ -358,7 +389,7 @@ __global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArg
       const uint32_t avail = ss.tail - ss.head, rk = mbcnt64(idle);
       if (!active && rk < avail) {
         slot = ss.at(ss.head + rk);
-        const float4 so = a.sh_o[slot], sd = a.sh_d[slot];
+        const float4 so = ldnt(a.sh_o + slot), sd = ldnt(a.sh_d + slot);
         r = make_ray(mk3(so.x, so.y, so.z), mk3(sd.x, sd.y, sd.z), 0.001f, so.w);
         seed = f2u(sd.w);
         node = 0; sp = 0;
@@ -415,7 +446,7 @@ __global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArg
     }
     if (state != 0) {
       if (state == 2) {  // reaches the light: the accumulation with the light's contribution
-        const float4 v = a.sh_acc[slot];
+        const float4 v = ldnt(a.sh_acc + slot);
         float* dst = reinterpret_cast<float*>(a.st_acc + slot);
         dst[0] = v.x; dst[1] = v.y; dst[2] = v.z;
       }
@@ -446,7 +477,7 @@ __global__ __launch_bounds__(256) void pt_wf_accumulate_kernel(WfArgs a, uint32_
   float sa = prev.w;
   for (uint32_t smp = 0; smp < a.batch; ++smp) {
     const uint32_t frame = a.frame0 + smp * a.stride;
-    const float4 s = a.st_acc[((size_t)t * a.batch + smp) * 64u + l];
+    const float4 s = ldnt(a.st_acc + ((size_t)t * a.batch + smp) * 64u + l);
     const v3 acc = mk3(s.x, s.y, s.z);
     if (mode == PTGS_ACCUM_SUM) {
       st = st + acc;
@@ -460,13 +491,13 @@ __global__ __launch_bounds__(256) void pt_wf_accumulate_kernel(WfArgs a, uint32_
   accum[pix] = make_float4(st.x, st.y, st.z, mode == PTGS_ACCUM_SUM ? sa : 1.0f);
 }
 
-// the per-workgroup partial counts of one call -> the context's counters (one workgroup), reset
+// the per-workgroup partial counts of one call -> the context's counters, reset for the next call
 __global__ __launch_bounds__(256) void pt_wf_fold_kernel(uint32_t* __restrict__ part, uint32_t stride,
                                                          unsigned long long* __restrict__ counters) {
   __shared__ unsigned long long s_sum[4];
   for (uint32_t k = 0; k < WF_NCNT; ++k) {
     unsigned long long v = 0;
-    for (uint32_t i = threadIdx.x; i < stride; i += 256u) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < stride; i += gridDim.x * 256u) {
       v += part[k * stride + i];
       part[k * stride + i] = 0u;
     }
@@ -476,7 +507,7 @@ __global__ __launch_bounds__(256) void pt_wf_fold_kernel(uint32_t* __restrict__ 
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned long long t = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-      if (t) counters[k] += t;
+      if (t) atomicAdd(counters + k, t);
     }
     __syncthreads();
   }
@@ -530,7 +561,9 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   a.tiles_x = (W + 7u) / 8u;
   a.stride = stride;
   const uint32_t tiles = a.tiles_x * ((row1 - row0 + 7u) / 8u);
-  const uint32_t bmax = std::min(batch_max, spp);
+  // samples per batch: up to batch_max, within ~2^25 slots (161 B each: 5.4 GB at the cap)
+  const uint32_t bcap = std::max(1u, (uint32_t)((1u << 25) / ((size_t)tiles * 64u)));
+  const uint32_t bmax = std::min({batch_max, spp, bcap});
   const size_t Pmax = (size_t)tiles * 64u * bmax;
   if (Pmax >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t grid_pmax = (uint32_t)((Pmax + 255u) / 256u);
@@ -538,7 +571,8 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   hipError_t e;
   // 10 float4 + 1 flag byte per slot
   if ((e = wf_ensure(w.slots, w.slots_bytes, Pmax * (10 * 16 + 1), false, s))) return e;
-  if ((e = wf_ensure(w.part, w.part_bytes, (size_t)WF_NCNT * a.part_stride * 4, true, s))) return e;
+  // partial counts [WF_NCNT][part_stride], then the per-depth "work pending" words (2 per depth)
+  if ((e = wf_ensure(w.part, w.part_bytes, ((size_t)WF_NCNT * a.part_stride + 64) * 4, true, s))) return e;
   float4* f = (float4*)w.slots;
   const size_t P = Pmax;
   a.ray_o = f; a.ray_d = f + P; a.hits = f + 2 * P;
@@ -546,6 +580,7 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   a.st_thr = f + 6 * P; a.st_w = f + 7 * P; a.st_acc = f + 8 * P;
   a.flags = (uint8_t*)(f + 10 * P);
   a.part = (uint32_t*)w.part;
+  a.live = a.part + (size_t)WF_NCNT * a.part_stride;
   const bool tex = sc.uses_textures != 0;
   auto ext = stats ? (tex ? pt_wf_extend_kernel<true, true> : pt_wf_extend_kernel<true, false>)
                    : (tex ? pt_wf_extend_kernel<false, true> : pt_wf_extend_kernel<false, false>);
@@ -561,14 +596,15 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
     const uint32_t grid_s = (a.slots + 4u * shade_run - 1u) / (4u * shade_run);
     hipLaunchKernelGGL(pt_wf_raygen_kernel, dim3(grid_p), dim3(256), 0, s, sc, cp, a);
     for (uint32_t d = 0; d < WF_MAX_DEPTH; ++d) {
-      hipLaunchKernelGGL(ext, dim3(grid_t), dim3(256), 0, s, sc, a, trace_run, refill);
+      hipLaunchKernelGGL(ext, dim3(grid_t), dim3(256), 0, s, sc, a, d, trace_run, refill);
       hipLaunchKernelGGL(shade, dim3(grid_s), dim3(256), 0, s, sc, cp, a, d, shade_run);
-      hipLaunchKernelGGL(shd, dim3(grid_t), dim3(256), 0, s, sc, a, trace_run, refill);
+      hipLaunchKernelGGL(shd, dim3(grid_t), dim3(256), 0, s, sc, a, d, trace_run, refill);
     }
     hipLaunchKernelGGL(pt_wf_accumulate_kernel, dim3((tiles * 64u + 255u) / 256u), dim3(256), 0, s, a, mode,
                        (float4*)accum);
   }
-  hipLaunchKernelGGL(pt_wf_fold_kernel, dim3(1), dim3(256), 0, s, a.part, a.part_stride, counters);
+  hipLaunchKernelGGL(pt_wf_fold_kernel, dim3(std::min(256u, (a.part_stride + 255u) / 256u)), dim3(256), 0, s, a.part,
+                     a.part_stride, counters);
   return hipGetLastError();
 }
 
