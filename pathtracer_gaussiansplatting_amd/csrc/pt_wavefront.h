@@ -41,6 +41,7 @@ struct WfArgs {
   uint32_t* part;                 // per-workgroup partial ray / sample counts [counter][block]
   uint32_t part_stride;
   uint32_t* live;                 // [2 d] extension rays pending at depth d, [2 d + 1] shadow rays
+  int* ovf;                       // traversal-stack overflow (PTGS_WF_LDS_STACK < PTGS_STACK)
 };
 
 // device buffers, grown on demand and reused across calls
@@ -49,6 +50,8 @@ struct WfWorkspace {
   size_t slots_bytes = 0;
   void* part = nullptr;
   size_t part_bytes = 0;
+  void* ovf = nullptr;
+  size_t ovf_bytes = 0;
 };
 
 void wf_workspace_free(WfWorkspace& w);

@@ -116,6 +116,34 @@ __device__ __forceinline__ void ss_fill(SlotStream& s, const uint8_t* __restrict
   wave_sync();
 }
 
+// Traversal stack of the extend / shadow kernels: the first WF_LDS_STACK entries in LDS (interleaved
+// by work-item, as pt_device.h), deeper entries (rare: C3's tree needs up to 34, C5's 38) in a
+// per-work-item global overflow area. A shorter LDS stack buys occupancy (LDS-bound otherwise).
+#ifndef PTGS_WF_LDS_EXT
+#define PTGS_WF_LDS_EXT PTGS_STACK  // extend kernel: LDS entries (39: 4 waves / SIMD, 86 VGPRs)
+#endif
+#ifndef PTGS_WF_LDS_SHADOW
+#define PTGS_WF_LDS_SHADOW 25       // shadow kernel: 25 entries: 6 waves / SIMD (73 VGPRs)
+#endif
+__host__ __device__ constexpr int wf_min_waves(int n) { return n <= 25 ? 6 : (n <= 31 ? 5 : 4); }
+template <int N>
+struct TravStack {
+  int* lds;       // this work-item's column
+  int* ovf;       // this work-item's overflow column (stride ostride)
+  uint32_t ostride;
+  int sp;
+  __device__ __forceinline__ void push(int v) {
+    if (N >= PTGS_STACK || sp < N) lds[sp * PTGS_BLOCK] = v;
+    else ovf[(size_t)(sp - N) * ostride] = v;
+    ++sp;
+  }
+  __device__ __forceinline__ int pop_nz() {  // sp > 0
+    --sp;
+    if (N >= PTGS_STACK || sp < N) return lds[sp * PTGS_BLOCK];
+    return ovf[(size_t)(sp - N) * ostride];
+  }
+};
+
 // block-level sum of v into part[k * stride + blockIdx.x] (plain read-modify-write: each block owns
 // its entry, successive launches are stream-ordered)
 __device__ __forceinline__ void block_count(uint32_t* __restrict__ part, uint32_t stride, int k, uint32_t v,
@@ -165,13 +193,17 @@ __global__ __launch_bounds__(256) void pt_wf_raygen_kernel(DevScene sc, CamParam
 // extend: closest hit of the pending extension rays (raygen_camera.rgen:51, pt_device.h trace_closest)
 // ------------------------------------------------------------------------------------------------
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(256, 4) void pt_wf_extend_kernel(DevScene sc, WfArgs a, uint32_t depth, uint32_t per_wave,
+__global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_extend_kernel(DevScene sc, WfArgs a, uint32_t depth, uint32_t per_wave,
                                                               uint32_t refill) {
   if (a.live[2u * depth] == 0u) return;  // no path reached this bounce (adaptive depth / RR ended them)
-  __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
+  __shared__ int s_stack[PTGS_WF_LDS_EXT * PTGS_BLOCK];
   __shared__ uint16_t s_ring[4][WF_RING];
   uint32_t* s_red = reinterpret_cast<uint32_t*>(s_ring);  // after the loop: the count reduction
-  int* stack = s_stack + threadIdx.x;
+  TravStack<PTGS_WF_LDS_EXT> st;
+  st.lds = s_stack + threadIdx.x;
+  st.ovf = a.ovf + blockIdx.x * 256u + threadIdx.x;
+  st.ostride = gridDim.x * 256u;
+  st.sp = 0;
   const uint32_t begin = (blockIdx.x * 4u + (threadIdx.x >> 6)) * per_wave;  // this wave's run of slots
   SlotStream ss;
   ss_init(ss, s_ring[threadIdx.x >> 6], begin, min(a.slots, begin + per_wave));
@@ -181,9 +213,9 @@ __global__ __launch_bounds__(256, 4) void pt_wf_extend_kernel(DevScene sc, WfArg
   uint32_t slot = 0, seed = 0;
   Ray r = make_ray(mk3(0.0f), mk3(1.0f), 0.001f, 10000.0f);
   Hit h; h.t = 0.f; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu; h.slot = 0;
-  int node = WF_DONE, sp = 0, leaf = WF_DONE;
-  auto push = [&](int v) { stack[(sp++) * PTGS_BLOCK] = v; };
-  auto pop = [&]() -> int { return sp ? stack[(--sp) * PTGS_BLOCK] : WF_DONE; };
+  int node = WF_DONE, leaf = WF_DONE;
+  auto push = [&](int v) { st.push(v); };
+  auto pop = [&]() -> int { return st.sp ? st.pop_nz() : WF_DONE; };
   for (;;) {
     // lanes whose ray finished take the next pending rays of the run, once `refill` of them are
     // idle (or none is busy): one refill's loads stall the wave, so they are batched
@@ -198,7 +230,7 @@ __global__ __launch_bounds__(256, 4) void pt_wf_extend_kernel(DevScene sc, WfArg
         r = make_ray(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), 0.001f, 10000.0f);
         seed = f2u(ro.w);
         h.t = r.tmax; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu;
-        node = 0; sp = 0; leaf = WF_DONE;
+        node = 0; st.sp = 0; leaf = WF_DONE;
         active = true;
       }
       ss.head += min(avail, nidle);
@@ -365,13 +397,17 @@ __global__ __launch_bounds__(256) void pt_wf_shade_kernel(DevScene sc, CamParams
 // shadow: any-hit of the pending NEE rays (pt_device.h trace_any); unoccluded -> the "visible" acc
 // ------------------------------------------------------------------------------------------------
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArgs a, uint32_t depth, uint32_t per_wave,
+__global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_shadow_kernel(DevScene sc, WfArgs a, uint32_t depth, uint32_t per_wave,
                                                               uint32_t refill) {
   if (a.live[2u * depth + 1u] == 0u) return;  // no shadow ray at this bounce
-  __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
+  __shared__ int s_stack[PTGS_WF_LDS_SHADOW * PTGS_BLOCK];
   __shared__ uint16_t s_ring[4][WF_RING];
   uint32_t* s_red = reinterpret_cast<uint32_t*>(s_ring);  // after the loop: the count reduction
-  int* stack = s_stack + threadIdx.x;
+  TravStack<PTGS_WF_LDS_SHADOW> st;
+  st.lds = s_stack + threadIdx.x;
+  st.ovf = a.ovf + blockIdx.x * 256u + threadIdx.x;
+  st.ostride = gridDim.x * 256u;
+  st.sp = 0;
   const uint32_t begin = (blockIdx.x * 4u + (threadIdx.x >> 6)) * per_wave;
   SlotStream ss;
   ss_init(ss, s_ring[threadIdx.x >> 6], begin, min(a.slots, begin + per_wave));
@@ -380,7 +416,7 @@ __global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArg
   bool active = false;
   uint32_t slot = 0, seed = 0;
   Ray r = make_ray(mk3(0.0f), mk3(1.0f), 0.001f, 1.0f);
-  int node = 0, sp = 0;
+  int node = 0;
   for (;;) {
     const unsigned long long idle = __ballot(!active);  // batched refill, as in the extend kernel
     const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -392,7 +428,7 @@ __global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArg
         const float4 so = ldnt(a.sh_o + slot), sd = ldnt(a.sh_d + slot);
         r = make_ray(mk3(so.x, so.y, so.z), mk3(sd.x, sd.y, sd.z), 0.001f, so.w);
         seed = f2u(sd.w);
-        node = 0; sp = 0;
+        node = 0; st.sp = 0;
         active = true;
       }
       ss.head += min(avail, nidle);
@@ -411,11 +447,11 @@ __global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArg
       for (int j = 0; j < 4; ++j)
         if (b.tn[j] != __builtin_huge_valf()) {
           if (!have) { nxt = b.c[j]; have = true; }
-          else stack[(sp++) * PTGS_BLOCK] = b.c[j];
+          else st.push(b.c[j]);
         }
       if (!have) {
-        if (sp == 0) { state = 2; break; }
-        node = stack[(--sp) * PTGS_BLOCK];
+        if (st.sp == 0) { state = 2; break; }
+        node = st.pop_nz();
         continue;
       }
       node = nxt;
@@ -440,8 +476,8 @@ __global__ __launch_bounds__(256, 4) void pt_wf_shadow_kernel(DevScene sc, WfArg
         break;
       }
       if (state == 0) {
-        if (sp == 0) state = 2;
-        else node = stack[(--sp) * PTGS_BLOCK];
+        if (st.sp == 0) state = 2;
+        else node = st.pop_nz();
       }
     }
     if (state != 0) {
@@ -528,7 +564,7 @@ static hipError_t wf_ensure(void*& p, size_t& have, size_t bytes, bool zero, hip
 }
 
 void wf_workspace_free(WfWorkspace& w) {
-  for (void** p : {&w.slots, &w.part})
+  for (void** p : {&w.slots, &w.part, &w.ovf})
     if (*p) (void)hipFree(*p);
   w = WfWorkspace{};
 }
@@ -573,6 +609,12 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   if ((e = wf_ensure(w.slots, w.slots_bytes, Pmax * (10 * 16 + 1), false, s))) return e;
   // partial counts [WF_NCNT][part_stride], then the per-depth "work pending" words (2 per depth)
   if ((e = wf_ensure(w.part, w.part_bytes, ((size_t)WF_NCNT * a.part_stride + 64) * 4, true, s))) return e;
+  {  // traversal-stack overflow: the entries beyond the LDS part, per work-item of the largest grid
+    const int deep = PTGS_STACK - std::min(PTGS_WF_LDS_EXT, PTGS_WF_LDS_SHADOW);
+    const size_t grid_tmax = (Pmax + 4u * trace_run - 1u) / (4u * trace_run);
+    if (deep > 0 && (e = wf_ensure(w.ovf, w.ovf_bytes, grid_tmax * 256u * (size_t)deep * 4u, false, s))) return e;
+    a.ovf = deep > 0 ? (int*)w.ovf : nullptr;
+  }
   float4* f = (float4*)w.slots;
   const size_t P = Pmax;
   a.ray_o = f; a.ray_d = f + P; a.hits = f + 2 * P;

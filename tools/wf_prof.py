@@ -14,7 +14,7 @@ SPP = int(os.environ.get("SPP", "64"))
 WF = os.environ.get("WF", "1") == "1"
 sc = Y.atrium_scene(target_tris=250_000, seed=2)
 sc.blue_noise = Y.blue_noise(1024)
-r = Renderer(0, wavefront=WF)
+r = Renderer(0, lib_path=os.environ.get("PTGS_LIB"), wavefront=WF)
 r.upload_scene(sc)
 pose = Camera(aspect=W / H).look_at([-15.0, 4.0, 5.0], [10.0, 3.0, -3.0])
 acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
