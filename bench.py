@@ -120,10 +120,11 @@ def main():
             dist.barrier()
 
     def reduce_to_root(t):
-        # RCCL reduce(SUM) to rank 0; the gloo rehearsal has no CUDA reduce: all-reduce instead
+        # RCCL reduce(SUM) to rank 0 through the library's communicator (ptgs_reduce_radiance); the gloo
+        # rehearsal (several ranks on one GPU) has no CUDA reduce: torch all-reduce instead
         if world > 1:
-            if dist.get_backend() == "nccl":
-                dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+            if native_comm:
+                r.reduce_radiance(t, root=0, stream=stream)
             else:
                 dist.all_reduce(t, op=dist.ReduceOp.SUM)
 
@@ -148,6 +149,11 @@ def main():
     W, H, SPP = args.width, args.height, args.spp
     r = Renderer(dev)
     stream = torch.cuda.current_stream()
+    from pathtracer_gaussiansplatting_amd import dist as D
+    # the library's own RCCL communicator (one rank per GPU): frame reduce and row gather through the C-ABI
+    native_comm = world > 1 and dist.get_backend() == "nccl"
+    if native_comm:
+        D.init_native_comm(r)
     out = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f32"}
 
@@ -282,7 +288,7 @@ def main():
 
     # ------------------------------------------------------------------ 3DGS (C2)
     if not args.no_gs:
-        g = Y.gaussians_c2(args.gaussians, seed=1 + rank)
+        g = Y.gaussians_c2(args.gaussians, seed=1)  # one scene: every rank holds all Gaussians
         dg = {k: torch.from_numpy(v).cuda() for k, v in g.items()}
         gpose = Camera(aspect=W / H).look_at([0.0, 0.0, 0.0], [0.0, 0.0, -1.0])
         from pathtracer_gaussiansplatting_amd import cornell_box_scene
@@ -292,11 +298,37 @@ def main():
             r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
         torch.cuda.synchronize()
         gsteps = max(args.steps, 100)  # ~0.1 ms per frame: enough frames for a stable mean
+        gs_rows = None
+        if world > 1:
+            # SURVEY 8e tile-row shard: rows balanced by a full frame's per-row pair counts (the same
+            # split on every rank), each rank renders its rows, rank 0 gathers them (W*H*16/G B each)
+            st0 = r.splat_gaussians(dg, gubo, W, H, img, want_stats=True, stream=stream)
+            b0 = r.splat_buffers()
+            rng = np.zeros(2 * b0.num_tiles, np.uint32)
+            r.copy_d2h(rng, b0.tile_ranges, rng.nbytes)
+            gs_rows = D.balanced_tile_rows(D.row_pairs_from_ranges(rng, st0.tiles_x), world, st0.tiles_x)
+            gs_px = [D.pixel_rows(t, H) for t in gs_rows]
+            hostimg = None if native_comm else torch.zeros((H, W, 4), dtype=torch.float32)
+
+        def gs_step():
+            if world == 1:
+                r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
+            elif native_comm:
+                D.render_gaussian_frame(r, dg, gubo, W, H, img, rank, world, stream=stream, tile_rows=gs_rows)
+            else:  # gloo rehearsal: the rows through host memory
+                if gs_rows[rank][1] > gs_rows[rank][0]:
+                    r.splat_gaussians(dg, gubo, W, H, img, tile_rows=gs_rows[rank], stream=stream)
+                p0, p1 = gs_px[rank]
+                hostimg[p0:p1].copy_(img[p0:p1])
+                D.gather_rows(hostimg, gs_px, dst=0)
+
+        for _ in range(max(args.warmup, 1)):
+            gs_step()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(gsteps):  # timed: no per-stage events, no stats read-back
-            r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
+            gs_step()
         torch.cuda.synchronize()
         barrier()
         gdt = max_over_ranks(time.perf_counter() - t0)
@@ -314,8 +346,11 @@ def main():
         b_gs = N * (56 + 48) + N * 48 + K * 12 + P * K * 24 + K * (4 + 48) + W * H * 16
         gms = gdt / gsteps * 1e3
         out["gs"] = {
-            "value": round(N * world / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
+            "value": round(N / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
             "workload": f"C2 3DGS forward: {N} synthetic Gaussians, {W}x{H}", "pairs_K": int(K),
+            "scaling": "strong", "parallelism": "single GPU" if world == 1 else
+            f"tile-row shard x{world} (rows balanced by pair counts: {gs_rows}) + row gather to rank 0"
+            + (" (ptgs_gather_rows, RCCL)" if native_comm else " (gloo rehearsal, host copies)"),
             "stages_ms": {k: round(float(v), 4) for k, v in
                           zip(["preprocess+count", "colscan", "scatter", "sort_large", "-", "sort_blend"], stages)
                           if k != "-"},
@@ -335,31 +370,32 @@ def main():
             "unit": "GB/s", "frac": round(b_alg / (blend_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "alg_bytes_per_launch": b_alg,
             "note": "algorithmic: 8-B key + 48-B blend record per (Gaussian, tile) pair + 16 B per pixel"})
-        out["gs"]["splat_pairs_per_s"] = round(K * world / (gdt / gsteps) / 1e9, 4)  # (Gaussian, tile) instances, G/s
-        # two frames in flight (the reference's MAX_FRAMES_IN_FLIGHT = 2): consecutive frames alternate
-        # between two contexts on two streams, so one frame's front end overlaps the other's blend
-        r2 = Renderer(dev)
-        s2 = torch.cuda.Stream()
-        img2 = torch.zeros_like(img)
-        pipes = [(r, stream, img), (r2, s2, img2)]
-        for k in range(4):
-            rk, sk, ik = pipes[k % 2]
-            rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(gsteps):
-            rk, sk, ik = pipes[k % 2]
-            rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
-        torch.cuda.synchronize()
-        barrier()
-        g2dt = max_over_ranks(time.perf_counter() - t0)
-        out["gs"]["two_in_flight"] = {"value": round(N * world / (g2dt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
-                                      "ms_per_step": round(g2dt / gsteps * 1e3, 4),
-                                      "note": "same frames, alternating between two contexts / streams"}
-        r2.close()
-        del img2
+        out["gs"]["splat_pairs_per_s"] = round(K / (gdt / gsteps) / 1e9, 4)  # (Gaussian, tile) instances, G/s
+        if world == 1:
+            # two frames in flight (the reference's MAX_FRAMES_IN_FLIGHT = 2): consecutive frames alternate
+            # between two contexts on two streams, so one frame's front end overlaps the other's blend
+            r2 = Renderer(dev)
+            s2 = torch.cuda.Stream()
+            img2 = torch.zeros_like(img)
+            pipes = [(r, stream, img), (r2, s2, img2)]
+            for k in range(4):
+                rk, sk, ik = pipes[k % 2]
+                rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
+            torch.cuda.synchronize()
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(gsteps):
+                rk, sk, ik = pipes[k % 2]
+                rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
+            torch.cuda.synchronize()
+            barrier()
+            g2dt = max_over_ranks(time.perf_counter() - t0)
+            out["gs"]["two_in_flight"] = {"value": round(N * world / (g2dt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
+                                          "ms_per_step": round(g2dt / gsteps * 1e3, 4),
+                                          "note": "same frames, alternating between two contexts / streams"}
+            r2.close()
+            del img2
         del dg
         # the same forward at the C4 hybrid's Gaussian count (1M), splat only
         if world == 1 and not args.no_gs_1m:

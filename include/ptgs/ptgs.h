@@ -429,6 +429,12 @@ int ptgs_comm_destroy(ptgs_ctx* ctx);
  * Stream-ordered on hip_stream. */
 int ptgs_reduce_radiance(ptgs_ctx* ctx, float* accum, size_t n_floats, int root, void* hip_stream);
 int ptgs_allreduce_radiance(ptgs_ctx* ctx, float* accum, size_t n_floats, void* hip_stream);
+/* Tile-row shards of the splat: rank g's pixel rows [row_ranges[2 g], row_ranges[2 g + 1]) of its
+ * RGBA32F width x height image are copied into the same rows of root's image (ncclSend / ncclRecv in
+ * one group: each rank moves only its own rows, W*H*16/G bytes, instead of a full-frame reduce).
+ * row_ranges holds every rank's range (2 x nranks, identical on all ranks). Stream-ordered. */
+int ptgs_gather_rows(ptgs_ctx* ctx, float* image, uint32_t width, uint32_t height, const uint32_t* row_ranges,
+                     int root, void* hip_stream);
 
 /* ---------------- output encode (blit rgba32f -> B8G8R8A8_SRGB, engine.cpp:2004-2020) --------- */
 /* rgba8 (device W*H u32, R in the low byte): linear -> sRGB8 of clamp(rgb,0,1), alpha 255. */

@@ -186,6 +186,7 @@ SYMBOLS = {
     "ptgs_comm_destroy": (_I, [_P]),
     "ptgs_reduce_radiance": (_I, [_P, _P, C.c_size_t, C.c_int, _P]),
     "ptgs_allreduce_radiance": (_I, [_P, _P, C.c_size_t, _P]),
+    "ptgs_gather_rows": (_I, [_P, _P, C.c_uint32, C.c_uint32, _P, C.c_int, _P]),
     "ptgs_splat_stage_ms": (_I, [_P, _FP]),
     "ptgs_encode_srgb8": (_I, [_P, _P, _U, _U, _P, _P]),
     "ptgs_device_alloc": (_I, [_P, C.c_size_t, C.POINTER(_P)]),

@@ -44,6 +44,7 @@ struct ptgs_ctx {
   SplatWorkspace* splat = nullptr;
   ptgs::WfWorkspace wf;  // wavefront path tracer buffers (PTGS_FLAG_PT_WAVEFRONT)
   void* comm = nullptr;  // RCCL communicator (ptgs_comm_create)
+  int comm_ranks = 0, comm_rank = 0;
 };
 
 namespace {
@@ -167,6 +168,8 @@ int ptgs_comm_create(ptgs_ctx* c, const uint8_t id[PTGS_COMM_ID_BYTES], int nran
   }
   int e = comm_create(id, nranks, rank, &c->comm);
   if (e) return fail(c, PTGS_EHIP, "ncclCommInitRank: %s", comm_error(e));
+  c->comm_ranks = nranks;
+  c->comm_rank = rank;
   return PTGS_OK;
 }
 
@@ -197,6 +200,22 @@ int ptgs_reduce_radiance(ptgs_ctx* c, float* accum, size_t n_floats, int root, v
 
 int ptgs_allreduce_radiance(ptgs_ctx* c, float* accum, size_t n_floats, void* stream) {
   return reduce_common(c, accum, n_floats, 0, true, stream);
+}
+
+int ptgs_gather_rows(ptgs_ctx* c, float* image, uint32_t width, uint32_t height, const uint32_t* row_ranges,
+                     int root, void* stream) {
+  if (!c || !image || !row_ranges) return PTGS_EINVAL;
+  if (!c->comm) return fail(c, PTGS_EINVAL, "no communicator (ptgs_comm_create)");
+  if (root < 0 || root >= c->comm_ranks) return fail(c, PTGS_EINVAL, "bad root %d", root);
+  if (!is_device_ptr(image)) return fail(c, PTGS_EINVAL, "image is not a device pointer");
+  for (int g = 0; g < c->comm_ranks; ++g)
+    if (row_ranges[2 * g] > row_ranges[2 * g + 1] || row_ranges[2 * g + 1] > height)
+      return fail(c, PTGS_EINVAL, "bad row range of rank %d", g);
+  HIPCHK(c, hipSetDevice(c->device));
+  int e = comm_gather_rows(c->comm, image, (size_t)width * 4u, row_ranges, c->comm_ranks, c->comm_rank, root,
+                           (hipStream_t)stream);
+  if (e) return fail(c, PTGS_EHIP, "ncclSend/ncclRecv: %s", comm_error(e));
+  return PTGS_OK;
 }
 
 const char* ptgs_last_error(const ptgs_ctx* c) { return c ? c->err.c_str() : "null context"; }

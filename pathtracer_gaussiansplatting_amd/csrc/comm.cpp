@@ -28,6 +28,10 @@ struct Rccl {
   ncclResult_t (*comm_destroy)(nccl_comm_t) = nullptr;
   ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, nccl_comm_t, hipStream_t) = nullptr;
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, nccl_comm_t, hipStream_t) = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, nccl_comm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, nccl_comm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   bool ok = false;
 };
@@ -50,7 +54,12 @@ Rccl& rccl() {
   r.reduce = (decltype(r.reduce))dlsym(r.so, "ncclReduce");
   r.all_reduce = (decltype(r.all_reduce))dlsym(r.so, "ncclAllReduce");
   r.error_string = (decltype(r.error_string))dlsym(r.so, "ncclGetErrorString");
-  r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.reduce && r.all_reduce && r.error_string;
+  r.send = (decltype(r.send))dlsym(r.so, "ncclSend");
+  r.recv = (decltype(r.recv))dlsym(r.so, "ncclRecv");
+  r.group_start = (decltype(r.group_start))dlsym(r.so, "ncclGroupStart");
+  r.group_end = (decltype(r.group_end))dlsym(r.so, "ncclGroupEnd");
+  r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.reduce && r.all_reduce && r.error_string &&
+         r.send && r.recv && r.group_start && r.group_end;
   return r;
 }
 
@@ -103,6 +112,28 @@ int comm_allreduce_sum(void* comm, float* buf, size_t n, hipStream_t s) {
   Rccl& r = rccl();
   if (!r.ok) return -1;
   return (int)r.all_reduce(buf, buf, n, ncclFloat32, ncclSum, (nccl_comm_t)comm, s);
+}
+
+// Every rank's own rows [range[2 g], range[2 g + 1]) of a row-major buffer (row_floats floats per
+// row) to the same rows of root's buffer: one ncclSend per rank, root posts the matching ncclRecv's,
+// all in one group (the disjoint tile-row shards of the splat: W*H*16/G bytes per rank instead of a
+// full-frame reduce).
+int comm_gather_rows(void* comm, float* buf, size_t row_floats, const uint32_t* range, int nranks, int rank, int root,
+                     hipStream_t s) {
+  Rccl& r = rccl();
+  if (!r.ok) return -1;
+  nccl_comm_t c = (nccl_comm_t)comm;
+  ncclResult_t e = r.group_start();
+  if (e != ncclSuccess) return (int)e;
+  for (int g = 0; g < nranks && e == ncclSuccess; ++g) {
+    const size_t off = (size_t)range[2 * g] * row_floats;
+    const size_t n = range[2 * g + 1] > range[2 * g] ? (size_t)(range[2 * g + 1] - range[2 * g]) * row_floats : 0;
+    if (g == root || n == 0) continue;
+    if (rank == g) e = r.send(buf + off, n, ncclFloat32, root, c, s);
+    else if (rank == root) e = r.recv(buf + off, n, ncclFloat32, g, c, s);
+  }
+  ncclResult_t e2 = r.group_end();
+  return (int)(e != ncclSuccess ? e : e2);
 }
 
 }  // namespace ptgs

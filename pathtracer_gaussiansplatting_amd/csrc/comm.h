@@ -15,5 +15,7 @@ int comm_create(const uint8_t* id, int nranks, int rank, void** comm);
 int comm_destroy(void* comm);
 int comm_reduce_sum(void* comm, float* buf, size_t n, int root, hipStream_t s);
 int comm_allreduce_sum(void* comm, float* buf, size_t n, hipStream_t s);
+int comm_gather_rows(void* comm, float* buf, size_t row_floats, const uint32_t* range, int nranks, int rank, int root,
+                     hipStream_t s);
 
 }  // namespace ptgs

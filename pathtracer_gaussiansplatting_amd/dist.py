@@ -8,8 +8,13 @@ mean = rgb / a. Equals the reference's running mean (raygen_camera.rgen:80-87) u
 summation order (~1e-7 relative); integer outputs (ray counts) are unaffected.
 
 3DGS — screen-tile shard. Gaussians are replicated; rank g renders tile rows [r0, r1) (global tile
-ids, so tile/bin indices are identical to the single-GPU frame) into a zeroed frame; the disjoint
-partial frames are summed with the same reduce (a gather of W*H*16/G bytes per rank).
+ids, so tile/bin indices are identical to the single-GPU frame); the root gathers every rank's rows
+(W*H*16/G bytes each: ptgs_gather_rows over RCCL send/recv with the library's communicator, or
+torch.distributed send/recv). Row ranges are balanced by per-tile-row pair counts (the work of the
+blend) from an earlier frame (balanced_tile_rows).
+
+With the library's own communicator (init_native_comm) the collectives run through the C-ABI
+(ptgs_reduce_radiance / ptgs_gather_rows); otherwise through torch.distributed.
 """
 from __future__ import annotations
 
@@ -30,6 +35,32 @@ def tile_row_shard(rank: int, world: int, height: int, tile: int = 16) -> tuple[
     return begin, end
 
 
+def balanced_tile_rows(row_pairs, world: int, tiles_x: int, tile_cost: float = 32.0) -> list[tuple[int, int]]:
+    """Contiguous tile-row ranges, one per rank, with about equal blend work: a tile row costs its
+    (Gaussian, tile) pairs plus tile_cost per tile (the per-tile fixed work). row_pairs: pairs per
+    tile row (e.g. from a previous frame's tile ranges)."""
+    import numpy as np
+    w = np.asarray(row_pairs, np.float64) + tile_cost * tiles_x
+    rows = len(w)
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    bounds = [0]
+    for g in range(1, world):
+        t = cum[-1] * g / world
+        b = int(np.searchsorted(cum, t, side="left"))
+        if b > 0 and (b > rows or t - cum[b - 1] < cum[b] - t):  # the nearer of the two boundaries
+            b -= 1
+        bounds.append(min(max(b, bounds[-1]), rows))
+    bounds.append(rows)
+    return [(bounds[g], bounds[g + 1]) for g in range(world)]
+
+
+def row_pairs_from_ranges(tile_ranges, tiles_x: int):
+    """Per-tile-row pair counts from a frame's tile ranges ((tiles, 2) uint32: [begin, end) per tile)."""
+    import numpy as np
+    r = np.asarray(tile_ranges, np.int64).reshape(-1, 2)
+    return (r[:, 1] - r[:, 0]).reshape(-1, tiles_x).sum(axis=1)
+
+
 def pixel_rows(tile_rows: tuple[int, int], height: int, tile: int = 16) -> tuple[int, int]:
     return min(tile_rows[0] * tile, height), min(tile_rows[1] * tile, height)
 
@@ -47,6 +78,27 @@ def all_reduce_sum(tensor, group=None):
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(tensor, op=dist.ReduceOp.SUM, group=group)
     return tensor
+
+
+def gather_rows(image, pixel_ranges, dst: int = 0, renderer=None, group=None):
+    """Every rank's pixel rows [r0, r1) of image ((H, W, 4) float32) to the same rows of dst's image.
+    Through the library's communicator when the renderer has one, else torch.distributed send/recv."""
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return image
+    if renderer is not None and getattr(renderer, "comm_world", 0) > 1:
+        renderer.gather_rows(image, pixel_ranges, root=dst)
+        return image
+    rank = dist.get_rank(group)
+    if rank == dst:
+        for g, (r0, r1) in enumerate(pixel_ranges):
+            if g != dst and r1 > r0:
+                dist.recv(image[r0:r1], src=g, group=group)
+    else:
+        r0, r1 = pixel_ranges[rank]
+        if r1 > r0:
+            dist.send(image[r0:r1].contiguous(), dst=dst, group=group)
+    return image
 
 
 def init_native_comm(renderer, group=None):
@@ -81,14 +133,19 @@ def render_path_traced_frame(renderer, ubo, width: int, height: int, accum, spp_
     accum.zero_()
     renderer.trace_camera(ubo, width, height, accum, spp=spp_per_rank, frame_stride=stride, mode=ACCUM_SUM,
                           stream=stream)
+    if getattr(renderer, "comm_world", 0) > 1:
+        renderer.reduce_radiance(accum, root=0, stream=stream)
+        return accum
     return reduce_sum(accum)
 
 
 def render_gaussian_frame(renderer, gaussians: dict, ubo, width: int, height: int, out, rank: int, world: int,
-                          bg=(0.0, 0.0, 0.0), stream=None):
-    """Tile-row-sharded 3DGS frame; the root gets the composed image."""
-    out.zero_()
-    rows = tile_row_shard(rank, world, height)
+                          bg=(0.0, 0.0, 0.0), stream=None, tile_rows=None):
+    """Tile-row-sharded 3DGS frame; the root gets the composed image. tile_rows: every rank's
+    (begin, end) tile rows (default: equal row counts, tile_row_shard)."""
+    if tile_rows is None:
+        tile_rows = [tile_row_shard(g, world, height) for g in range(world)]
+    rows = tile_rows[rank]
     if rows[1] > rows[0]:
         renderer.splat_gaussians(gaussians, ubo, width, height, out, bg=bg, tile_rows=rows, stream=stream)
-    return reduce_sum(out)
+    return gather_rows(out, [pixel_rows(r, height) for r in tile_rows], dst=0, renderer=renderer)

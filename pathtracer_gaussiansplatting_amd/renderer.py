@@ -146,9 +146,11 @@ class Renderer:
     def comm_create(self, unique_id: bytes, nranks: int, rank: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self._chk(self.lib.ptgs_comm_create(self._h, buf, nranks, rank), "ptgs_comm_create")
+        self.comm_world = nranks
 
     def comm_destroy(self):
         self._chk(self.lib.ptgs_comm_destroy(self._h), "ptgs_comm_destroy")
+        self.comm_world = 0
 
     def reduce_radiance(self, accum, root: int = 0, stream=None):
         rc = self.lib.ptgs_reduce_radiance(self._h, _ptr(accum), accum.numel(), root, _stream(stream))
@@ -157,6 +159,14 @@ class Renderer:
     def allreduce_radiance(self, accum, stream=None):
         rc = self.lib.ptgs_allreduce_radiance(self._h, _ptr(accum), accum.numel(), _stream(stream))
         self._chk(rc, "ptgs_allreduce_radiance")
+
+    def gather_rows(self, image, row_ranges, root: int = 0, stream=None):
+        """Every rank's pixel rows [r0, r1) of the (H, W, 4) float32 image to root (ptgs_gather_rows);
+        row_ranges: one (r0, r1) per rank, identical on every rank."""
+        H, W = int(image.shape[0]), int(image.shape[1])
+        rr = np.asarray(row_ranges, np.uint32).reshape(-1)
+        rc = self.lib.ptgs_gather_rows(self._h, _ptr(image), W, H, rr.ctypes.data, root, _stream(stream))
+        self._chk(rc, "ptgs_gather_rows")
 
     def set_flags(self, flags: int):
         self._flags = flags

@@ -96,3 +96,99 @@ def test_shard_helpers():
     assert D.tile_row_shard(9, 10, 64) == (4, 4)  # more ranks than rows: empty shard
     with pytest.raises(ValueError):
         D.sample_shard(3, 3)
+
+
+class _OracleRenderer:
+    """Test stand-in for one rank's GPU renderer (the trace_camera / splat_gaussians interface of
+    pathtracer_gaussiansplatting_amd.Renderer), backed by the CPU oracle: the product's sharding
+    helpers (dist.render_path_traced_frame / render_gaussian_frame) run unchanged on top of it."""
+
+    def __init__(self, scene):
+        import oracle
+        self.oracle = oracle
+        self.scene = scene
+        self.comm_world = 0  # no native communicator: the torch.distributed (gloo) collectives
+
+    def trace_camera(self, ubo, width, height, accum, spp=1, frame_stride=1, mode=0, rows=None, stream=None):
+        acc = accum.numpy()
+        self.oracle.trace_camera(self.scene.desc(), ubo, width, height, acc, spp=spp, frame_stride=frame_stride,
+                                 mode=mode, rows=rows)
+
+    def splat_gaussians(self, g, ubo, width, height, out, bg=(0.0, 0.0, 0.0), tile_rows=None, stream=None,
+                        want_stats=False):
+        ref = self.oracle.splat_gaussians({k: v.numpy() for k, v in g.items()}, ubo, width, height, bg=bg,
+                                          tile_rows=tile_rows)
+        r0, r1 = (0, height) if tile_rows is None else (min(tile_rows[0] * 16, height), min(tile_rows[1] * 16, height))
+        out[r0:r1] = torch.from_numpy(ref["image"][r0:r1])
+        return ref
+
+
+def _frame_worker(rank, world, port, q):
+    """dist.render_path_traced_frame + dist.render_gaussian_frame (balanced tile rows, row gather)."""
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        import scenes_util as U
+        from pathtracer_gaussiansplatting_amd import Camera, make_ubo
+        from pathtracer_gaussiansplatting_amd import dist as D
+        from pathtracer_gaussiansplatting_amd import synthetic as Y
+
+        sc = U.cornell()
+        r = _OracleRenderer(sc)
+        W, H, spp = 24, 20, 2
+        acc = torch.zeros((H, W, 4), dtype=torch.float32)
+        D.render_path_traced_frame(r, make_ubo(U.cornell_pose(W / H), sc, 0), W, H, acc, spp, rank, world)
+        # 3DGS: rows balanced by the pair counts of a full-frame pass (every rank computes the same split)
+        GW, GH = 96, 70
+        g = {k: torch.from_numpy(v) for k, v in Y.gaussians_c2(1500, seed=5).items()}
+        gu = make_ubo(Camera(aspect=GW / GH).look_at([0, 0, 0], [0, 0, -1]), sc, 0)
+        full = oracle.splat_gaussians({k: v.numpy() for k, v in g.items()}, gu, GW, GH)
+        tiles_x = (GW + 15) // 16
+        rows = D.balanced_tile_rows(D.row_pairs_from_ranges(full["ranges"], tiles_x), world, tiles_x)
+        out = torch.full((GH, GW, 4), -1.0, dtype=torch.float32)  # rows not rendered here stay -1 unless gathered
+        D.render_gaussian_frame(r, g, gu, GW, GH, out, rank, world, tile_rows=rows)
+        if rank == 0:
+            ref = np.zeros((H, W, 4), np.float32)
+            oracle.trace_camera(sc.desc(), make_ubo(U.cornell_pose(W / H), sc, 0), W, H, ref, spp=spp * world)
+            err = U.rel_l2(D.resolve_mean(acc).numpy()[..., :3], ref[..., :3])
+            q.put(("ok", err, float(acc[..., 3].min()), float(acc[..., 3].max()),
+                   bool(np.array_equal(out.numpy(), full["image"])), rows))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", traceback.format_exc()))
+
+
+def test_dist_render_frames_gloo():
+    """world 2: the product's frame helpers (sample shard + reduce; balanced tile rows + row gather)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_frame_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+    assert res[0] == "ok", res[1]
+    _, err, cmin, cmax, gs_equal, rows = res
+    assert err < 1e-5, err
+    assert cmin == cmax == 2 * world
+    assert gs_equal, rows
+    assert rows[0][0] == 0 and rows[-1][1] == 5 and rows[0][1] == rows[1][0]
+
+
+def test_balanced_tile_rows():
+    from pathtracer_gaussiansplatting_amd import dist as D
+    rows = D.balanced_tile_rows([0, 0, 100, 500, 500, 100, 0, 0], 3, 10)
+    assert rows == [(0, 3), (3, 5), (5, 8)]
+    even = D.balanced_tile_rows([5] * 68, 8, 120)
+    assert [e - b for b, e in even] == [9, 8, 9, 8, 9, 8, 9, 8]
+    assert D.balanced_tile_rows([1, 2], 4, 1) == [(0, 1), (1, 1), (1, 2), (2, 2)]
+    assert list(D.row_pairs_from_ranges(np.array([[0, 3], [3, 3], [3, 10], [10, 12]], np.uint32), 2)) == [3, 9]

@@ -136,8 +136,14 @@ def test_native_rccl_reduce_single_rank(renderer):
     ref = x.clone()
     renderer.reduce_radiance(x, root=0)
     renderer.allreduce_radiance(x)
+    img = torch.arange(16 * 8 * 4, dtype=torch.float32, device="cuda").reshape(16, 8, 4)
+    renderer.gather_rows(img, [(0, 16)], root=0)  # ptgs_gather_rows: the root's own rows stay in place
     torch.cuda.synchronize()
     assert torch.equal(x, ref)
+    assert torch.equal(img.flatten(), torch.arange(16 * 8 * 4, dtype=torch.float32, device="cuda"))
+    from pathtracer_gaussiansplatting_amd import PtgsError
+    with pytest.raises(PtgsError):
+        renderer.gather_rows(img, [(0, 17)], root=0)  # rows beyond the image
     renderer.comm_destroy()
 
 
