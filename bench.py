@@ -400,6 +400,7 @@ def main():
         # the same forward at the C4 hybrid's Gaussian count (1M), splat only
         if world == 1 and not args.no_gs_1m:
             g1 = {k: torch.from_numpy(v).cuda() for k, v in Y.gaussians_c2(args.hybrid_gaussians, seed=3).items()}
+            r.splat_gaussians(g1, gubo, W, H, img, want_stats=True, stream=stream)  # sizes the pair buffer
             for _ in range(2):
                 r.splat_gaussians(g1, gubo, W, H, img, stream=stream)
             torch.cuda.synchronize()
@@ -433,7 +434,11 @@ def main():
             img5 = torch.zeros((H5, W5, 4), dtype=torch.float32, device="cuda")
             g5pose = Camera(aspect=W5 / H5).look_at([0.0, 0.0, 0.0], [0.0, 0.0, -1.0])
             g5ubo = make_ubo(g5pose, cornell_box_scene(), 0)
-            for _ in range(3):  # the sort sizes follow the previous frames' tiles
+            # untimed: one frame with stats sizes the pair buffer for this frame's K (160M pairs; without
+            # stats an over-capacity frame is skipped and the buffer grows on the next call), then the
+            # sort sizes follow the previous frames' tiles
+            r.splat_gaussians(g5, g5ubo, W5, H5, img5, want_stats=True, stream=stream)
+            for _ in range(3):
                 r.splat_gaussians(g5, g5ubo, W5, H5, img5, stream=stream)
             torch.cuda.synchronize()
             n5 = 5

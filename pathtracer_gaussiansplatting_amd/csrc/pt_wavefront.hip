@@ -119,6 +119,9 @@ __device__ __forceinline__ void ss_fill(SlotStream& s, const uint8_t* __restrict
 // Traversal stack of the extend / shadow kernels: the first WF_LDS_STACK entries in LDS (interleaved
 // by work-item, as pt_device.h), deeper entries (rare: C3's tree needs up to 34, C5's 38) in a
 // per-work-item global overflow area. A shorter LDS stack buys occupancy (LDS-bound otherwise).
+#ifndef PTGS_WF_AH_CALL
+#define PTGS_WF_AH_CALL true  // textured any-hit out of line (pt_device.h anyhit_accept_call)
+#endif
 #ifndef PTGS_WF_LDS_EXT
 #define PTGS_WF_LDS_EXT PTGS_STACK  // extend kernel: LDS entries (39: 4 waves / SIMD, 86 VGPRs)
 #endif
@@ -258,11 +261,11 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_exte
       if (__all(leaf != WF_DONE || node == WF_DONE)) break;
     }
     if (leaf != WF_DONE) {
-      leaf_closest<STATS, TEX, true>(sc, r, leaf, h, seed, tc);
+      leaf_closest<STATS, TEX, PTGS_WF_AH_CALL>(sc, r, leaf, h, seed, tc);
       leaf = WF_DONE;
     }
     if (node < 0) {
-      leaf_closest<STATS, TEX, true>(sc, r, node, h, seed, tc);
+      leaf_closest<STATS, TEX, PTGS_WF_AH_CALL>(sc, r, node, h, seed, tc);
       node = pop();
     }
     if (node == WF_DONE) {
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_shad
         if (!tri_isect(r, mk3(ta.x, ta.y, ta.z), mk3(tb.x, tb.y, tb.z), mk3(tcv.x, tcv.y, tcv.z), t, u, v)) continue;
         if (!(t >= r.tmin && t <= r.tmax)) continue;
         if (sc.has_transparent && (sc.tri_flags[start + k] & 1u)) {
-          const bool acc = TEX ? anyhit_accept_call(sc, f2u(ta.w), f2u(tb.w), u, v, seed, f2u(tcv.w))
+          const bool acc = (TEX && PTGS_WF_AH_CALL) ? anyhit_accept_call(sc, f2u(ta.w), f2u(tb.w), u, v, seed, f2u(tcv.w))
                                : anyhit_accept<TEX>(sc, f2u(ta.w), f2u(tb.w), u, v, seed, f2u(tcv.w));
           if (!acc) continue;
         }
@@ -607,7 +610,7 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   hipError_t e;
   // 10 float4 + 1 flag byte per slot
   if ((e = wf_ensure(w.slots, w.slots_bytes, Pmax * (10 * 16 + 1), false, s))) return e;
-  // partial counts [WF_NCNT][part_stride], then the per-depth "work pending" words (2 per depth)
+  // the per-depth "work pending" words (2 per depth), then the partial counts [WF_NCNT][part_stride]
   if ((e = wf_ensure(w.part, w.part_bytes, ((size_t)WF_NCNT * a.part_stride + 64) * 4, true, s))) return e;
   {  // traversal-stack overflow: the entries beyond the LDS part, per work-item of the largest grid
     const int deep = PTGS_STACK - std::min(PTGS_WF_LDS_EXT, PTGS_WF_LDS_SHADOW);
@@ -621,8 +624,10 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   a.sh_o = f + 3 * P; a.sh_d = f + 4 * P; a.sh_acc = f + 5 * P;
   a.st_thr = f + 6 * P; a.st_w = f + 7 * P; a.st_acc = f + 8 * P;
   a.flags = (uint8_t*)(f + 10 * P);
-  a.part = (uint32_t*)w.part;
-  a.live = a.part + (size_t)WF_NCNT * a.part_stride;
+  // the "work pending" words first: at a fixed offset, so a later call with a larger grid (stride)
+  // never counts a previous call's flags as partial ray counts
+  a.live = (uint32_t*)w.part;
+  a.part = a.live + 64;
   const bool tex = sc.uses_textures != 0;
   auto ext = stats ? (tex ? pt_wf_extend_kernel<true, true> : pt_wf_extend_kernel<true, false>)
                    : (tex ? pt_wf_extend_kernel<false, true> : pt_wf_extend_kernel<false, false>);

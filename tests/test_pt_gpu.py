@@ -57,6 +57,19 @@ def test_cornell_256_1spp(pt, oracle_lib):
     print(f"cornell rel L2 {err:.2e}, {nd} pixels differ, ext {sg.extension_rays} shadow {sg.shadow_rays}")
 
 
+def test_counts_after_a_smaller_call(pt, oracle_lib):
+    """Ray counts of a call that follows a smaller one on the same context (the wavefront workspace
+    is reused with a larger grid: a previous call's per-bounce work flags must not be counted as
+    partial ray counts)."""
+    sc = U.cornell()
+    ubo = make_ubo(U.cornell_pose(), sc, 0)
+    _gpu_render(pt, sc, ubo, 24, 24, 3)
+    g, sg = _gpu_render(pt, sc, ubo, 192, 192, 2)
+    o, so = _oracle_render(oracle_lib, sc, ubo, 192, 192, 2)
+    _compare(g, o, sg, so)
+    assert sg.samples == 192 * 192 * 2
+
+
 def test_cornell_running_mean(pt, oracle_lib):
     """frames 3..6 on top of an existing accumulator (mix(prev, cur, 1/(n+1)), raygen_camera.rgen:80-87)."""
     sc = U.cornell()
