@@ -48,6 +48,19 @@ namespace G = ptgs::glm;
 
 namespace {
 
+// unaligned little-endian loads from accessor data
+inline uint32_t ld_u16(const uint8_t* p) {
+  uint16_t v;
+  memcpy(&v, p, 2);
+  return v;
+}
+inline uint32_t ld_u32(const uint8_t* p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+
+
 struct LoadError {
   std::string msg;
 };
@@ -286,10 +299,10 @@ G::mat4 node_local(const JVal& n) {
 
 int scene_index(const Model& m) {
   const JVal* scenes = m.doc.get("scenes");
-  if (!scenes || scenes->size() == 0) fail("glTF has no scenes!");
+  if (!scenes || scenes->kind != JVal::ARR || scenes->arr.empty()) fail("glTF has no scenes!");
   int ds = ptgs::jint(m.doc.get("scene"), -1);
   int si = ds > -1 ? ds : 0;
-  if ((size_t)si >= scenes->size()) fail("default scene index out of range");
+  if ((size_t)si >= scenes->arr.size()) fail("default scene index out of range");
   return si;
 }
 
@@ -315,19 +328,22 @@ void global_transforms(const Model& m, std::vector<G::mat4>& globals) {
       if (pathk == "translation") {
         Model::View v = m.view(out_acc, 12, 12, "animation output");
         if (!v.count) continue;
-        const float* f = (const float*)v.p;
+        float f[3];
+        memcpy(f, v.p, 12);  // (accessor data need not be 4-byte aligned in a damaged file)
         anim[node].t = G::v3(f[0], f[1], f[2]);
         anim[node].ht = true;
       } else if (pathk == "rotation") {
         Model::View v = m.view(out_acc, 16, 16, "animation output");
         if (!v.count) continue;
-        const float* f = (const float*)v.p;
+        float f[4];
+        memcpy(f, v.p, 16);
         anim[node].r.x = f[0]; anim[node].r.y = f[1]; anim[node].r.z = f[2]; anim[node].r.w = f[3];
         anim[node].hr = true;
       } else if (pathk == "scale") {
         Model::View v = m.view(out_acc, 12, 12, "animation output");
         if (!v.count) continue;
-        const float* f = (const float*)v.p;
+        float f[3];
+        memcpy(f, v.p, 12);
         anim[node].s = G::v3(f[0], f[1], f[2]);
         anim[node].hs = true;
       }
@@ -369,7 +385,8 @@ void global_transforms(const Model& m, std::vector<G::mat4>& globals) {
     for (size_t i = 0; ch && i < ch->size(); ++i) walk(ptgs::jint(ch->at(i), -1), global);
     on_stack[ni] = 0;
   };
-  const JVal& sc = m.doc.get("scenes")->arr[(size_t)scene_index(m)];
+  const size_t si = (size_t)scene_index(m);  // (validates "scenes" before it is dereferenced)
+  const JVal& sc = m.doc.get("scenes")->arr[si];
   const JVal* roots = sc.get("nodes");
   for (size_t i = 0; roots && i < roots->size(); ++i) walk(ptgs::jint(roots->at(i), -1), G::identity4());
 }
@@ -670,8 +687,8 @@ struct Loader {
       Model::View iv = m.view(ia, es, es, "indices");
       src_idx.resize(iv.count);
       for (size_t i = 0; i < iv.count; ++i) {
-        if (ct == 5123) src_idx[i] = ((const uint16_t*)iv.p)[i];
-        else if (ct == 5125) src_idx[i] = ((const uint32_t*)iv.p)[i];
+        if (ct == 5123) src_idx[i] = ld_u16(iv.p + 2 * i);
+        else if (ct == 5125) src_idx[i] = ld_u32(iv.p + 4 * i);
         else src_idx[i] = iv.p[i];
       }
     } else {
@@ -718,7 +735,7 @@ struct Loader {
         if (idx >= jnt.count || idx >= wgt.count) fail("skin attribute index out of range");
         uint32_t j[4];
         const uint8_t* jp = jnt.p + idx * jnt.stride;
-        for (int k = 0; k < 4; ++k) j[k] = jnt.ctype == 5123 ? ((const uint16_t*)jp)[k] : jp[k];
+        for (int k = 0; k < 4; ++k) j[k] = jnt.ctype == 5123 ? ld_u16(jp + 2 * k) : jp[k];
         float w[4] = {1.0f, 0.0f, 0.0f, 0.0f};
         if (wgt.ctype == 5126) memcpy(w, wgt.p + idx * wgt.stride, 16);
         float sum = ((w[0] + w[1]) + w[2]) + w[3];

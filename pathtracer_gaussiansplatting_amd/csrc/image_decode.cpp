@@ -11,8 +11,12 @@
 //         "fancy" triangle-filter chroma upsampling for 2x1 / 1x2 / 2x2 and nearest otherwise,
 //         with stb's row-phase state machine; Adobe APP14 transform 0 -> CMYK (x*k/255 "blinn"),
 //         2 -> YCCK, component ids 'R','G','B' (or no JFIF and transform 0) -> RGB stored directly.
-// The decoders are written from the format specifications (PNG ISO/IEC 15948, JPEG ITU T.81);
-// only the numeric conventions above are taken from the reference's decoder. Inflate is zlib's.
+// The parsers (chunks, markers, Huffman / progressive scans, Adam7) are written from the format
+// specifications (PNG ISO/IEC 15948, JPEG ITU T.81). The arithmetic that decides pixel values
+// follows stb_image (the reference's vendored Helpers/stb_image.h, public domain) because the texels
+// must equal stbi_load's: the integer IDCT (idct8x8 restates stbi__idct_block, stb_image.h:2426-2520:
+// same constants, biases and output order), the fixed-point YCbCr->RGB and the chroma resamplers.
+// Inflate is zlib's.
 #include "image_decode.h"
 
 #include <zlib.h>
@@ -21,16 +25,29 @@
 #include <climits>
 #include <cstdio>
 #include <cstring>
-#include <fstream>
-#include <iterator>
+#include <sys/stat.h>
 
 namespace ptgs {
 
+// regular files only (a directory opens as a stream and then throws from its first read); no
+// exceptions (callers are behind the C-ABI)
 bool read_file(const std::string& path, std::vector<uint8_t>& bytes) {
-  std::ifstream f(path, std::ios::binary);
-  if (!f.is_open()) return false;
-  bytes.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
-  return true;
+  bytes.clear();
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  struct stat st;
+  bool ok = fstat(fileno(f), &st) == 0 && S_ISREG(st.st_mode) && st.st_size >= 0;
+  if (ok) {
+    try {
+      bytes.resize((size_t)st.st_size);
+    } catch (...) {
+      ok = false;
+    }
+  }
+  if (ok && !bytes.empty()) ok = fread(bytes.data(), 1, bytes.size(), f) == bytes.size();
+  fclose(f);
+  if (!ok) bytes.clear();
+  return ok;
 }
 
 namespace {
@@ -347,6 +364,7 @@ bool build_huff(HuffTable& t, const uint8_t counts[16], const uint8_t* vals, int
     int c = counts[len - 1];
     if (c) {
       for (int i = 0; i < c; ++i, ++k, ++code) {
+        if (code >= (1 << len) || k >= nvals) return false;  // over-subscribed lengths (corrupt DHT)
         if (len <= 9) {
           int shift = 9 - len;
           for (int f = 0; f < (1 << shift); ++f) t.look[(code << shift) | f] = (uint16_t)(len << 8 | t.vals[k]);
@@ -489,18 +507,21 @@ class JpegDecoder {
   void output(DecodedImage& out);
 };
 
-// jidctint-style 8x8 integer IDCT on dequantised coefficients; writes 8 bytes per row
-inline int fx(float x) { return (int)(x * 4096 + 0.5); }
+// jidctint-style 8x8 integer IDCT on dequantised coefficients (stb_image.h stbi__idct_block:
+// same constants, biases and output order); writes 8 bytes per row. 64-bit intermediates: a corrupt
+// stream can carry coefficients whose 32-bit products overflow (valid data never does, so the
+// results equal the 32-bit ones)
+inline int64_t fx(float x) { return (int64_t)(x * 4096 + 0.5); }
 #define PTGS_IDCT_1D(s0, s1, s2, s3, s4, s5, s6, s7)                                        \
-  int e2 = s2, e6 = s6;                                                                    \
-  int z1 = (e2 + e6) * fx(0.5411961f);                                                     \
-  int ev2 = z1 + e6 * fx(-1.847759065f);                                                   \
-  int ev3 = z1 + e2 * fx(0.765366865f);                                                    \
-  int ev0 = (s0 + s4) * 4096, ev1 = (s0 - s4) * 4096;                                      \
-  int a0 = ev0 + ev3, a3 = ev0 - ev3, a1 = ev1 + ev2, a2 = ev1 - ev2;                      \
-  int o7 = s7, o5 = s5, o3 = s3, o1 = s1;                                                  \
-  int q3 = o7 + o3, q4 = o5 + o1, q1 = o7 + o1, q2 = o5 + o3;                              \
-  int q5 = (q3 + q4) * fx(1.175875602f);                                                   \
+  int64_t e2 = s2, e6 = s6;                                                                    \
+  int64_t z1 = (e2 + e6) * fx(0.5411961f);                                                     \
+  int64_t ev2 = z1 + e6 * fx(-1.847759065f);                                                   \
+  int64_t ev3 = z1 + e2 * fx(0.765366865f);                                                    \
+  int64_t ev0 = (s0 + s4) * 4096, ev1 = (s0 - s4) * 4096;                                      \
+  int64_t a0 = ev0 + ev3, a3 = ev0 - ev3, a1 = ev1 + ev2, a2 = ev1 - ev2;                      \
+  int64_t o7 = s7, o5 = s5, o3 = s3, o1 = s1;                                                  \
+  int64_t q3 = o7 + o3, q4 = o5 + o1, q1 = o7 + o1, q2 = o5 + o3;                              \
+  int64_t q5 = (q3 + q4) * fx(1.175875602f);                                                   \
   o7 = o7 * fx(0.298631336f);                                                              \
   o5 = o5 * fx(2.053119869f);                                                              \
   o3 = o3 * fx(3.072711026f);                                                              \
@@ -514,10 +535,10 @@ inline int fx(float x) { return (int)(x * 4096 + 0.5); }
   o5 += q2 + q4;                                                                           \
   o7 += q1 + q3;
 
-inline uint8_t clamp255(int x) { return (uint8_t)(x < 0 ? 0 : (x > 255 ? 255 : x)); }
+inline uint8_t clamp255(int64_t x) { return (uint8_t)(x < 0 ? 0 : (x > 255 ? 255 : x)); }
 
 void idct8x8(uint8_t* out, int stride, const int16_t* d) {
-  int tmp[64];
+  int64_t tmp[64];
   for (int c = 0; c < 8; ++c) {
     const int16_t* col = d + c;
     PTGS_IDCT_1D(col[0], col[8], col[16], col[24], col[32], col[40], col[48], col[56])
@@ -532,10 +553,10 @@ void idct8x8(uint8_t* out, int stride, const int16_t* d) {
     tmp[c + 32] = (a3 - o7) >> 10;
   }
   for (int r = 0; r < 8; ++r) {
-    const int* t = tmp + 8 * r;
+    const int64_t* t = tmp + 8 * r;
     uint8_t* o = out + (size_t)r * stride;
     PTGS_IDCT_1D(t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7])
-    const int bias = 65536 + (128 << 17);
+    const int64_t bias = 65536 + (128 << 17);
     a0 += bias; a1 += bias; a2 += bias; a3 += bias;
     o[0] = clamp255((a0 + o1) >> 17);
     o[7] = clamp255((a0 - o1) >> 17);

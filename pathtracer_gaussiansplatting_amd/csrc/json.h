@@ -152,15 +152,24 @@ struct JParser {
     else if (lit("false")) { v.kind = JVal::BOOL; v.b = false; }
     else if (lit("null")) { v.kind = JVal::NUL; }
     else {
-      const char* s = p;
+      // the number's characters (JSON grammar: sign, digits, '.', exponent), copied into a bounded
+      // NUL-terminated buffer: the document itself is not NUL-terminated, strtod must not run past it
+      const char* q = p;
+      while (q < end && q - p < 63 &&
+             ((*q >= '0' && *q <= '9') || *q == '-' || *q == '+' || *q == '.' || *q == 'e' || *q == 'E'))
+        ++q;
+      char buf[64];
+      const size_t len = (size_t)(q - p);
+      memcpy(buf, p, len);
+      buf[len] = '\0';
       char* e = nullptr;
-      v.num = strtod(p, &e);
-      if (e == p) { ok = false; --depth; return v; }
+      v.num = strtod(buf, &e);
+      if (e == buf) { ok = false; --depth; return v; }
       v.kind = JVal::NUM;
       v.is_int = true;
-      for (const char* q = s; q < e; ++q)
-        if (*q == '.' || *q == 'e' || *q == 'E') v.is_int = false;
-      p = e;
+      for (const char* c = buf; c < e; ++c)
+        if (*c == '.' || *c == 'e' || *c == 'E') v.is_int = false;
+      p += e - buf;
     }
     --depth;
     return v;

@@ -78,7 +78,7 @@ extern "C" int ptgs_read_ply(const char* path, float* xyz, float* normals, uint8
       if (!memcmp(s + i, tag, 10)) {
         size_t j = i + 10;
         while (j < n && s[j] != '\n') ++j;
-        hdr_end = j + 1;
+        hdr_end = std::min(j + 1, n);  // (a header that ends the file without a newline)
         break;
       }
   }
@@ -124,6 +124,7 @@ extern "C" int ptgs_read_ply(const char* path, float* xyz, float* normals, uint8
   if (vi < 0) return PTGS_EIO;
   const Elem& V = elems[vi];
   if (V.count > 0xFFFFFFFFull) return PTGS_ERANGE;
+  if (V.props.empty()) return PTGS_EIO;  // (rows of no bytes: the count would be unbounded)
   // header counts must fit the body (checked before the count query returns, so a caller never
   // sizes buffers from an impossible count): ASCII rows take at least one byte each, binary rows
   // exactly their size (elements before "vertex" must have fixed-size rows)

@@ -12,6 +12,7 @@
 
 #include "../../include/ptgs/ptgs_host.h"
 #include "hostmath.h"
+#include "image_decode.h"
 #include "json.h"
 #include "scene_builder.h"
 
@@ -152,11 +153,9 @@ const char* ptgs_builder_last_error(const ptgs_scene_builder* b) { return b ? b-
 // Engine::createRTBox, engine.cpp:181-335
 int ptgs_builder_add_rtbox_json(ptgs_scene_builder* b, const char* path) {
   if (!b || !path) return PTGS_EINVAL;
-  std::ifstream f(path);
-  if (!f.is_open()) { b->err = std::string("cannot open ") + path; return PTGS_EIO; }
-  std::stringstream ss;
-  ss << f.rdbuf();
-  std::string text = ss.str();
+  std::vector<uint8_t> bytes;
+  if (!ptgs::read_file(path, bytes)) { b->err = std::string("cannot read ") + path; return PTGS_EIO; }
+  const std::string text(bytes.begin(), bytes.end());
   JVal cfg;
   if (!ptgs::parse_json(text.data(), text.size(), cfg) || cfg.kind != JVal::OBJ) { b->err = std::string("bad JSON in ") + path; return PTGS_EIO; }
   const JVal* jpos = cfg.get("position");
