@@ -203,8 +203,10 @@ void oracle_camera_toroidal(float alpha_deg, float beta_deg, float radius, float
     if (be < 0.0f) be += 360.0f;
     const float D2R = 0.01745329251994329576923690768489f;
     float a = al * D2R, b = be * D2R;
-    v3 pos = add(mul(V(cosf(a), 0.0f, sinf(a)), radius), V(0.0f, height, 0.0f));
-    v3 fwd = g_norm(V(-cosf(a), 0.0f, -sinf(a)));
+    /* camera.cpp:205,208: unqualified cos / sin of a float resolve to the double ::cos / ::sin */
+    const float ca = (float)cos((double)a), sa = (float)sin((double)a);
+    v3 pos = add(mul(V(ca, 0.0f, sa), radius), V(0.0f, height, 0.0f));
+    v3 fwd = g_norm(V(-ca, 0.0f, -sa));
     v3 up = V(0.0f, 1.0f, 0.0f);
     v3 right = g_norm(g_cross(fwd, up));
     v3 nf = g_rotate(b, right, fwd);

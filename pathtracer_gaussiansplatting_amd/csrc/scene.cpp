@@ -128,8 +128,13 @@ int ptgs_camera_toroidal(float alpha_deg, float beta_deg, float radius, float he
   float beta = gmod(beta_deg, 360.0f);
   if (beta < 0.0f) beta += 360.0f;
   float a = radians(alpha), b = radians(beta);
-  f3 pos = add(mul(f3{std::cos(a), 0.0f, std::sin(a)}, radius), f3{0.0f, height, 0.0f});
-  f3 base_forward = normalize(f3{-std::cos(a), 0.0f, -std::sin(a)});
+  // camera.cpp:205,208 call cos / sin unqualified on a float: with no float overload in the global
+  // namespace that is the C library's double ::cos / ::sin, rounded to float by the vec3 constructor
+  // (glm::rotate below uses the float std::cos / std::sin). With float cosf / sinf here pose 36 of
+  // dataset/transforms_test.json came out 2 ulps off; with double all 64 golden poses are exact.
+  const float ca = (float)std::cos((double)a), sa = (float)std::sin((double)a);
+  f3 pos = add(mul(f3{ca, 0.0f, sa}, radius), f3{0.0f, height, 0.0f});
+  f3 base_forward = normalize(f3{-ca, 0.0f, -sa});
   f3 base_up = {0.0f, 1.0f, 0.0f};
   f3 right = normalize(cross(base_forward, base_up));
   f3 new_forward = rotate_dir(b, right, base_forward);
