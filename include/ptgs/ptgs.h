@@ -236,6 +236,16 @@ const char* ptgs_device_arch(void);
 /* Replaces buildBlas/initStaticTlas (engine.cpp:534-655, :1385-1520) + the descriptor uploads. */
 int ptgs_scene_upload(ptgs_ctx* ctx, const ptgs_scene_desc* desc);
 int ptgs_scene_get_info(const ptgs_ctx* ctx, ptgs_scene_info* out);
+/* Debug / parity access to the uploaded acceleration structure (device pointers owned by the
+ * context, valid until the next upload): 4-wide nodes (bvh.h layout, 128 B each) and the triangle
+ * records in leaf order (48 B each: (v0, mesh) (v1 - v0, prim) (v2 - v0, gid)). */
+typedef struct ptgs_bvh_buffers {
+    const float* nodes;
+    uint32_t num_nodes;
+    const float* triangles;
+    uint32_t num_triangles;
+} ptgs_bvh_buffers;
+int ptgs_scene_get_bvh(const ptgs_ctx* ctx, ptgs_bvh_buffers* out);
 
 /* ---------------- path tracer (raygen_camera.rgen + closesthit/miss/shadow) ---------------- */
 
@@ -283,9 +293,10 @@ typedef struct ptgs_trace_stats {
 
 #define PTGS_FLAG_COUNT_TRAVERSAL 1u /* instrumented kernels: node / triangle / hit counters */
 #define PTGS_FLAG_TIME_STAGES 2u     /* hipEvent timing of the splat pipeline stages */
-#define PTGS_FLAG_GPU_BVH 4u         /* ptgs_scene_upload builds the BVH on the GPU (LBVH; fast rebuilds,
-                                      * slower traversal than the default host SAH build); falls back to
-                                      * the host build when the tree exceeds the traversal stack depth */
+#define PTGS_FLAG_GPU_BVH 4u         /* ptgs_scene_upload builds the BVH on the GPU: the host builder's
+                                      * binned SAH run on the device (the same tree: same node boxes and
+                                      * leaf ranges, so the same traversal cost); falls back to the host
+                                      * build for inputs it does not handle */
 #define PTGS_FLAG_SPLAT_PUBLISH 8u   /* ptgs_splat_gaussians also writes the sorted keys / values of every
                                       * tile (ptgs_splat_get_buffers; parity tests): off in production,
                                       * the blend needs neither */
@@ -293,6 +304,9 @@ typedef struct ptgs_trace_stats {
                                       * shade / shadow / accumulate stages over compacted ray queues)
                                       * instead of the one-kernel-per-frame path loop; same image, same
                                       * ray counts */
+#define PTGS_FLAG_GPU_LBVH 32u       /* with PTGS_FLAG_GPU_BVH: a linear BVH (Morton order, Karras 2012)
+                                      * instead: fastest rebuilds, slower traversal; host fallback when it
+                                      * exceeds the traversal stack depth */
 int ptgs_set_flags(ptgs_ctx* ctx, uint32_t flags);
 int ptgs_stats_reset(ptgs_ctx* ctx, void* hip_stream);
 int ptgs_stats_read(ptgs_ctx* ctx, ptgs_trace_stats* out); /* synchronises the context's device */

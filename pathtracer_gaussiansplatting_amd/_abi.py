@@ -21,6 +21,7 @@ ACCUM_SUM = 1
 FLAG_COUNT_TRAVERSAL = 1
 FLAG_TIME_STAGES = 2
 FLAG_GPU_BVH = 4
+FLAG_GPU_LBVH = 32
 FLAG_SPLAT_PUBLISH = 8
 FLAG_PT_WAVEFRONT = 16
 
@@ -150,6 +151,11 @@ class SplatBuffers(C.Structure):
                 ("num_rendered", C.c_uint32), ("num_tiles", C.c_uint32)]
 
 
+class BvhBuffers(C.Structure):
+    _fields_ = [("nodes", C.c_void_p), ("num_nodes", C.c_uint32), ("triangles", C.c_void_p),
+                ("num_triangles", C.c_uint32)]
+
+
 assert C.sizeof(Ubo) == 192 and C.sizeof(RayPush) == 80
 
 # (name, restype, argtypes) of every symbol include/ptgs/*.h declares
@@ -166,6 +172,7 @@ SYMBOLS = {
     "ptgs_last_error": (C.c_char_p, [_P]),
     "ptgs_scene_upload": (_I, [_P, C.POINTER(SceneDesc)]),
     "ptgs_scene_get_info": (_I, [_P, C.POINTER(SceneInfo)]),
+    "ptgs_scene_get_bvh": (_I, [_P, C.POINTER(BvhBuffers)]),
     "ptgs_trace_camera": (_I, [_P, C.POINTER(Ubo), _U, _U, _P, _U, _U, _U, _P]),
     "ptgs_trace_camera_rows": (_I, [_P, C.POINTER(Ubo), _U, _U, _U, _U, _P, _U, _U, _U, _P]),
     "ptgs_trace_torus": (_I, [_P, C.POINTER(Ubo), C.POINTER(RayPush), _P, _U, _P, _P]),

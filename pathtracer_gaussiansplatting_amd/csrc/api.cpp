@@ -293,7 +293,8 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
   if ((c->flags & PTGS_FLAG_GPU_BVH) && tris.size() >= 16) {
     GpuBvh g;
     float ms = 0.0f;
-    hipError_t e = build_bvh_gpu(tris, PTGS_STACK - 1, g, &ms);
+    hipError_t e = (c->flags & PTGS_FLAG_GPU_LBVH) ? build_bvh_gpu(tris, PTGS_STACK - 1, g, &ms)
+                                                  : build_bvh_sah_gpu(tris, PTGS_BVH_LEAF, PTGS_STACK - 1, g, &ms);
     if (e == hipSuccess) {  // 4-wide collapse on the host (D2H of the BVH2 nodes, collapse, H2D)
       auto t0 = std::chrono::steady_clock::now();
       std::vector<float> n2((size_t)g.num_nodes * 16), n4;
@@ -317,7 +318,7 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
       s.tri_flags = g.tri_flags;
       c->info.num_bvh_nodes = g.num_nodes;
       c->info.bvh_depth = g.depth;
-      c->info.max_leaf_size = 4;
+      c->info.max_leaf_size = (c->flags & PTGS_FLAG_GPU_LBVH) ? 4u : g.max_leaf;
       c->info.build_ms = ms;
       c->info.device_bytes += (size_t)g.num_nodes * 128 + tris.size() * 52;
       built = true;
@@ -396,6 +397,16 @@ int ptgs_scene_get_info(const ptgs_ctx* c, ptgs_scene_info* out) {
   if (!c || !out) return PTGS_EINVAL;
   if (!c->has_scene) return PTGS_ENOSCENE;
   *out = c->info;
+  return PTGS_OK;
+}
+
+int ptgs_scene_get_bvh(const ptgs_ctx* c, ptgs_bvh_buffers* out) {
+  if (!c || !out) return PTGS_EINVAL;
+  if (!c->has_scene) return PTGS_ENOSCENE;
+  out->nodes = (const float*)c->dsc.nodes;
+  out->num_nodes = c->info.num_bvh_nodes;
+  out->triangles = (const float*)c->dsc.tris;
+  out->num_triangles = c->info.num_triangles;
   return PTGS_OK;
 }
 

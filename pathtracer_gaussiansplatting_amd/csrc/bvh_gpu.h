@@ -15,10 +15,18 @@ struct GpuBvh {
   uint32_t* tri_flags = nullptr;
   uint32_t num_nodes = 0;
   uint32_t depth = 0;
+  uint32_t max_leaf = 0;
 };
 
 // n >= 2 triangles. hipErrorNotSupported: the tree is deeper than max_depth (out holds it; free it
 // and build on the host). build_ms: device time of the build kernels.
 hipError_t build_bvh_gpu(const std::vector<BuildTri>& tris, uint32_t max_depth, GpuBvh& out, float* build_ms);
+
+// GPU binned-SAH builder (bvh_sah_gpu.hip): the host builder's algorithm (build_bvh, bvh.cpp) with
+// the same float operations, so the tree (node boxes, leaf ranges) is the host tree; BVH2 node
+// numbering and the triangle order inside a leaf differ. hipErrorNotSupported: unsupported input
+// (build on the host).
+hipError_t build_bvh_sah_gpu(const std::vector<BuildTri>& tris, uint32_t max_leaf, uint32_t max_depth, GpuBvh& out,
+                             float* build_ms);
 
 }  // namespace ptgs

@@ -16,7 +16,7 @@ import ctypes as C
 import numpy as np
 
 from . import _abi
-from ._abi import Gaussians, RayPush, SceneInfo, SplatBuffers, SplatStats, TraceStats, Ubo
+from ._abi import BvhBuffers, Gaussians, RayPush, SceneInfo, SplatBuffers, SplatStats, TraceStats, Ubo
 
 
 def _ptr(x) -> int:
@@ -213,6 +213,12 @@ class Renderer:
                                            t1, _ptr(out), C.byref(st) if want_stats else None, _stream(stream))
         self._chk(rc, "ptgs_splat_gaussians")
         return st if want_stats else None
+
+    def bvh_buffers(self) -> BvhBuffers:
+        """Device pointers of the uploaded 4-wide BVH nodes and leaf-order triangle records."""
+        b = BvhBuffers()
+        self._chk(self.lib.ptgs_scene_get_bvh(self._h, C.byref(b)), "ptgs_scene_get_bvh")
+        return b
 
     def splat_buffers(self) -> SplatBuffers:
         b = SplatBuffers()

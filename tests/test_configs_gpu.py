@@ -156,3 +156,27 @@ def test_c5_10m_gaussians_1m_tris_4k(renderer, oracle_lib):
     st = _hybrid_case(renderer, oracle_lib, sc, 3840, 2160, 4, 10_000_000, 5,
                       tile_bands=[(0, 5), (66, 68)], trace_rows=[(0, 80), (1056, 1088)])
     print(f"C5: K={st.num_rendered}")
+
+
+def test_c5_mesh_gpu_sah_build(renderer):
+    """C5's 1M-triangle mesh built on the GPU (PTGS_FLAG_GPU_BVH, bvh_sah_gpu.hip): the 4-wide nodes
+    equal the host SAH build's word for word and every leaf holds the same triangles."""
+    from test_pt_gpu import _bvh_arrays, _leaf_sets_equal
+
+    from pathtracer_gaussiansplatting_amd import FLAG_GPU_BVH
+    sc = U.atrium(1_000_000)
+    renderer.upload_scene(sc)
+    info_h = renderer.scene_info()
+    nodes_h, tris_h = _bvh_arrays(renderer)
+    renderer.set_flags(FLAG_GPU_BVH)
+    try:
+        renderer.upload_scene(sc)
+        info_g = renderer.scene_info()
+        nodes_g, tris_g = _bvh_arrays(renderer)
+    finally:
+        renderer.set_flags(0)
+    assert info_g.num_triangles == info_h.num_triangles >= 1_000_000
+    assert np.array_equal(nodes_g, nodes_h), f"{int(np.count_nonzero(np.any(nodes_g != nodes_h, 1)))} nodes differ"
+    assert _leaf_sets_equal(nodes_h, tris_h, tris_g)
+    print(f"1M tris: host SAH {info_h.build_ms:.1f} ms, GPU SAH {info_g.build_ms:.2f} ms, "
+          f"{info_g.num_bvh_nodes} 4-wide nodes, depth {info_g.bvh_depth}")

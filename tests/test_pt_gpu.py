@@ -160,27 +160,82 @@ def test_native_rccl_reduce_single_rank(renderer):
     renderer.comm_destroy()
 
 
+def _bvh_arrays(renderer):
+    """(BVH4 nodes as u32 [n, 32], triangle records as u32 [t, 12]) of the uploaded scene."""
+    bb = renderer.bvh_buffers()
+    nodes = np.zeros((bb.num_nodes, 32), np.uint32)
+    tris = np.zeros((bb.num_triangles, 12), np.uint32)
+    renderer.copy_d2h(nodes, bb.nodes, nodes.nbytes)
+    renderer.copy_d2h(tris, bb.triangles, tris.nbytes)
+    return nodes, tris
+
+
+def _leaf_sets_equal(nodes, tris_a, tris_b):
+    """Every leaf range of the 4-wide nodes holds the same triangle records in both arrays (the
+    order inside a leaf may differ)."""
+    links = nodes[:, 24:28].view(np.int32).reshape(-1)
+    boxes_lo_x = nodes[:, 0:4].view(np.float32).reshape(-1)
+    leaves = links[(links < 0) & (boxes_lo_x < 1e29)]
+    L = (~leaves).astype(np.uint32)
+    first, count = L & 0x07FFFFFF, (L >> 27) + 1
+    for f, c in zip(first.tolist(), count.tolist()):
+        ra = tris_a[f:f + c]
+        rb = tris_b[f:f + c]
+        ka = np.lexsort(ra.T[::-1])
+        kb = np.lexsort(rb.T[::-1])
+        if not np.array_equal(ra[ka], rb[kb]):
+            return False
+    return int(count.sum()) == tris_a.shape[0]
+
+
 @pytest.mark.parametrize("scene", ["features", "atrium"])
-def test_gpu_bvh_builder_same_image(renderer, scene):
-    """PTGS_FLAG_GPU_BVH (LBVH built on the GPU) renders the image of the host SAH BVH bit for bit:
-    hits do not depend on the tree (closest-hit tie rule, conservative boxes)."""
+def test_gpu_sah_bvh_is_the_host_tree(renderer, oracle_lib, scene):
+    """PTGS_FLAG_GPU_BVH: the binned-SAH build on the GPU (bvh_sah_gpu.hip) reproduces the host build
+    (bvh.cpp): the 4-wide nodes are identical word for word (boxes, links, leaf ranges) and every
+    leaf holds the same triangles; the image equals the oracle's bit for bit."""
     from pathtracer_gaussiansplatting_amd import FLAG_GPU_BVH
     sc = U.features() if scene == "features" else U.atrium()
     pose = U.cornell_pose(160 / 120) if scene == "features" else U.atrium_pose()
     ubo = make_ubo(pose, sc, 0, ambient=(0.3, 0.4, 0.5, 1.0))
-    host, st_h = _gpu_render(renderer, sc, ubo, 160, 120, 2)
+    renderer.upload_scene(sc)
     info_h = renderer.scene_info()
+    nodes_h, tris_h = _bvh_arrays(renderer)
     renderer.set_flags(FLAG_GPU_BVH)
+    try:
+        gpu, st_g = _gpu_render(renderer, sc, ubo, 160, 120, 2)
+        info_g = renderer.scene_info()
+        nodes_g, tris_g = _bvh_arrays(renderer)
+    finally:
+        renderer.set_flags(0)
+    assert (info_g.num_bvh_nodes, info_g.bvh_depth) == (info_h.num_bvh_nodes, info_h.bvh_depth)
+    assert np.array_equal(nodes_g, nodes_h), f"{int(np.count_nonzero(np.any(nodes_g != nodes_h, 1)))} nodes differ"
+    assert _leaf_sets_equal(nodes_h, tris_h, tris_g)
+    o, so = _oracle_render(oracle_lib, sc, ubo, 160, 120, 2)
+    _compare(gpu, o, st_g, so)
+    assert np.array_equal(gpu, o)
+    print(f"{scene}: host SAH {info_h.build_ms:.1f} ms, GPU SAH {info_g.build_ms:.2f} ms "
+          f"({info_g.num_bvh_nodes} 4-wide nodes, depth {info_g.bvh_depth})")
+
+
+@pytest.mark.parametrize("scene", ["features", "atrium"])
+def test_gpu_lbvh_vs_oracle(renderer, oracle_lib, scene):
+    """PTGS_FLAG_GPU_BVH | PTGS_FLAG_GPU_LBVH (linear BVH on the GPU): the image and ray counts equal
+    the oracle's (its own median-split BVH): hits do not depend on the tree (closest-hit tie rule,
+    conservative boxes)."""
+    from pathtracer_gaussiansplatting_amd import FLAG_GPU_BVH, FLAG_GPU_LBVH
+    sc = U.features() if scene == "features" else U.atrium()
+    pose = U.cornell_pose(160 / 120) if scene == "features" else U.atrium_pose()
+    ubo = make_ubo(pose, sc, 0, ambient=(0.3, 0.4, 0.5, 1.0))
+    renderer.set_flags(FLAG_GPU_BVH | FLAG_GPU_LBVH)
     try:
         gpu, st_g = _gpu_render(renderer, sc, ubo, 160, 120, 2)
         info_g = renderer.scene_info()
     finally:
         renderer.set_flags(0)
-    assert np.array_equal(gpu, host)
-    assert st_g.extension_rays == st_h.extension_rays and st_g.shadow_rays == st_h.shadow_rays
-    assert info_g.num_triangles == info_h.num_triangles and info_g.bvh_depth <= 31
-    print(f"{scene}: host SAH {info_h.build_ms:.1f} ms ({info_h.num_bvh_nodes} nodes, depth {info_h.bvh_depth}), "
-          f"GPU LBVH {info_g.build_ms:.2f} ms ({info_g.num_bvh_nodes} nodes, depth {info_g.bvh_depth})")
+    o, so = _oracle_render(oracle_lib, sc, ubo, 160, 120, 2)
+    _compare(gpu, o, st_g, so)
+    assert np.array_equal(gpu, o)
+    print(f"{scene}: GPU LBVH {info_g.build_ms:.2f} ms ({info_g.num_bvh_nodes} nodes, depth {info_g.bvh_depth})")
 
 
 def test_ingested_scene_json(pt, oracle_lib):
