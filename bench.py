@@ -142,7 +142,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
-    from pathtracer_gaussiansplatting_amd import (ACCUM_RUNNING_MEAN, ACCUM_SUM, FLAG_COUNT_TRAVERSAL, FLAG_GPU_BVH,
+    from pathtracer_gaussiansplatting_amd import (ACCUM_RUNNING_MEAN, ACCUM_SUM, FLAG_COUNT_TRAVERSAL, FLAG_GPU_BVH, FLAG_GPU_LBVH,
                                                   FLAG_TIME_STAGES, Camera, Renderer, make_ubo)
     from pathtracer_gaussiansplatting_amd import synthetic as Y
 
@@ -264,25 +264,31 @@ def main():
             out["pt_wavefront"] = {"value": round(sum_over_ranks(float(wst.extension_rays + wst.shadow_rays)) / wdt / 1e6,
                                                   3), "unit": "Mrays/s", "ms_per_step": round(wdt / args.steps * 1e3, 3),
                                    "note": "same C3 frames through the wavefront stages (PTGS_FLAG_PT_WAVEFRONT)"}
-        # the GPU LBVH builder (PTGS_FLAG_GPU_BVH) on the same scene: build time and one traced frame
+        # the GPU BVH builders on the same scene: build time and one traced frame each. PTGS_FLAG_GPU_BVH
+        # is the host's binned SAH run on the GPU (the same tree: the same traversal cost);
+        # PTGS_FLAG_GPU_LBVH the linear BVH (fastest rebuilds, weaker tree)
         if world == 1 and not args.no_gpu_bvh:
-            r.set_flags(FLAG_GPU_BVH)
-            r.upload_scene(scene)  # first build pays hipCUB / module first-use costs
-            ginfo = r.upload_scene(scene)
-            r.set_flags(0)
-            pt_step()
-            torch.cuda.synchronize()
-            r.stats_reset(stream)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            pt_step()
-            torch.cuda.synchronize()
-            gdt_pt = time.perf_counter() - t0
-            gst = r.stats()
-            out["bvh_gpu"] = {"build_ms": round(float(ginfo.build_ms), 3), "nodes": int(ginfo.num_bvh_nodes),
-                              "depth": int(ginfo.bvh_depth),
-                              "mrays_per_s": round((gst.extension_rays + gst.shadow_rays) / gdt_pt / 1e6, 2),
-                              "note": "LBVH built on the GPU (fast rebuilds); the headline value uses the host SAH BVH"}
+            out["bvh_gpu"] = {}
+            for key, flags, note in (("sah", FLAG_GPU_BVH, "host binned-SAH algorithm on the GPU: the host tree"),
+                                     ("lbvh", FLAG_GPU_BVH | FLAG_GPU_LBVH, "linear BVH (Morton order)")):
+                r.set_flags(flags)
+                r.upload_scene(scene)  # first build pays module first-use costs
+                ginfo = r.upload_scene(scene)
+                r.set_flags(0)
+                pt_step()
+                torch.cuda.synchronize()
+                r.stats_reset(stream)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                pt_step()
+                torch.cuda.synchronize()
+                gdt_pt = time.perf_counter() - t0
+                gst = r.stats()
+                out["bvh_gpu"][key] = {"build_ms": round(float(ginfo.build_ms), 3), "nodes": int(ginfo.num_bvh_nodes),
+                                       "depth": int(ginfo.bvh_depth),
+                                       "mrays_per_s": round((gst.extension_rays + gst.shadow_rays) / gdt_pt / 1e6, 2),
+                                       "note": note}
+            out["bvh_gpu"]["host_sah_build_ms"] = round(float(info.build_ms), 3)
             r.upload_scene(scene)  # back to the SAH tree for the legs below
         del accum
 

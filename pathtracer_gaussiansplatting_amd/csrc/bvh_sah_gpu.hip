@@ -40,7 +40,10 @@ namespace {
 
 constexpr int NB = 32;               // bins per axis (bvh.cpp NB)
 constexpr uint32_t CH = 2048;        // references per phase-A chunk
-constexpr uint32_t GS_SAH_T = 4096;  // phase-A / phase-B boundary (task size)
+#ifndef PTGS_SAH_T
+#define PTGS_SAH_T 1024
+#endif
+constexpr uint32_t GS_SAH_T = PTGS_SAH_T;  // phase-A / phase-B boundary (task size)
 constexpr int BT = 256;              // threads per workgroup
 constexpr uint32_t EMPTY_LO = 0xFFFFFFFFu, EMPTY_HI = 0u;
 constexpr int SB_STACK = 48;         // phase-B LDS task stack (depth <= max_depth + 1)
@@ -145,42 +148,59 @@ __device__ __forceinline__ int32_t leaf_link(uint32_t begin, uint32_t count) {  
   return ~(int32_t)(((count - 1u) << 27) | begin);
 }
 
-// The host's SAH sweep for one axis (bvh.cpp :108-118): best (cost, bin) with cost strictly smaller
-// than any earlier candidate of this axis
-__device__ void sweep_axis(const uint32_t* bins /* [NB][7] */, float& best_cost, int& best_bin) {
-  float rarea[NB];
-  uint32_t rcnt[NB];
-  Box acc;
-  box_reset(acc);
-  uint32_t c = 0;
-  for (int k = NB - 1; k > 0; --k) {
-    const uint32_t* b = bins + 7 * k;
-    if (b[6]) {
-      Box bb;
-      for (int a = 0; a < 3; ++a) { bb.lo[a] = o2f(b[a]); bb.hi[a] = o2f(b[3 + a]); }
-      box_grow(acc, bb);
+// The host's SAH sweeps (bvh.cpp :98-118) by 32 lanes of one wave, one axis per pass: prefix / suffix unions by
+// shuffle scans (min / max are exact, so every union equals the sequential one), the costs of the
+// host formula per split candidate, then the first minimum in (axis, bin) order (the host's strict
+// "<" across bins, then across axes). Called by every lane of one wave; lanes >= 32 idle.
+__device__ __noinline__ void sweep_wave(const uint32_t* bins /* [3][NB][7] */, const bool on[3], float& best_cost, int& best_axis,
+                           int& best_bin) {
+  const int lane = (int)(threadIdx.x & 63u), k = lane & 31;
+  float bc = __builtin_huge_valf();
+  int bi = 0x7fffffff;
+  for (int a = 0; a < 3; ++a) {
+    if (!on[a]) continue;
+    const uint32_t* b = bins + (a * NB + k) * 7;
+    const uint32_t cnt = b[6];
+    Box me;
+    if (cnt) {
+      for (int q = 0; q < 3; ++q) { me.lo[q] = o2f(b[q]); me.hi[q] = o2f(b[3 + q]); }
+    } else {
+      box_reset(me);
     }
-    c += b[6];
-    rarea[k] = box_area(acc);
-    rcnt[k] = c;
-  }
-  box_reset(acc);
-  c = 0;
-  best_cost = __builtin_huge_valf();
-  best_bin = -1;
-  for (int k = 0; k < NB - 1; ++k) {
-    const uint32_t* b = bins + 7 * k;
-    if (b[6]) {
-      Box bb;
-      for (int a = 0; a < 3; ++a) { bb.lo[a] = o2f(b[a]); bb.hi[a] = o2f(b[3 + a]); }
-      box_grow(acc, bb);
+    Box pre = me, suf = me;
+    uint32_t pc = cnt, sc = cnt;
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+      Box up, dn;
+      for (int q = 0; q < 3; ++q) {
+        up.lo[q] = __shfl_up(pre.lo[q], off, 32); up.hi[q] = __shfl_up(pre.hi[q], off, 32);
+        dn.lo[q] = __shfl_down(suf.lo[q], off, 32); dn.hi[q] = __shfl_down(suf.hi[q], off, 32);
+      }
+      const uint32_t uc = __shfl_up(pc, off, 32), dc = __shfl_down(sc, off, 32);
+      if (k >= off) { box_grow(pre, up); pc += uc; }
+      if (k + off < 32) { box_grow(suf, dn); sc += dc; }
     }
-    c += b[6];
-    if (c == 0 || rcnt[k + 1] == 0) continue;
-    const float cost = box_area(acc) * (float)c + rarea[k + 1] * (float)rcnt[k + 1];
-    if (cost < best_cost) { best_cost = cost; best_bin = k; }
+    // candidate k: left = bins [0, k], right = bins [k + 1, NB)
+    Box rs;
+    for (int q = 0; q < 3; ++q) { rs.lo[q] = __shfl_down(suf.lo[q], 1, 32); rs.hi[q] = __shfl_down(suf.hi[q], 1, 32); }
+    const uint32_t rc = __shfl_down(sc, 1, 32);
+    if (k < NB - 1 && pc != 0 && rc != 0) {
+      const float cost = box_area(pre) * (float)pc + box_area(rs) * (float)rc;
+      if (cost < bc) { bc = cost; bi = a * NB + k; }
+    }
   }
+  // first minimum over (cost, axis * NB + bin)
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) {
+    const float oc = __shfl_xor(bc, off, 32);
+    const int oi = __shfl_xor(bi, off, 32);
+    if (oc < bc || (oc == bc && oi < bi)) { bc = oc; bi = oi; }
+  }
+  best_cost = bc;
+  best_axis = bi == 0x7fffffff ? -1 : bi / NB;
+  best_bin = bi == 0x7fffffff ? -1 : bi % NB;
 }
+
 __device__ __forceinline__ Box bins_union(const uint32_t* bins, int k0, int k1) {  // bins [k0, k1]
   Box acc;
   box_reset(acc);
@@ -257,7 +277,17 @@ __global__ void sah_refs_kernel(const BuildTri* __restrict__ tris, uint32_t n, R
     for (int a = 0; a < 3; ++a) { cl[a] = fminf(cl[a], __shfl_xor(cl[a], off, 64)); chh[a] = fmaxf(chh[a], __shfl_xor(chh[a], off, 64)); }
     ma = fmaxf(ma, __shfl_xor(ma, off, 64));
   }
+  __shared__ float s_r[4][7];
   if ((threadIdx.x & 63u) == 0) {
+    for (int a = 0; a < 3; ++a) { s_r[threadIdx.x >> 6][a] = cl[a]; s_r[threadIdx.x >> 6][3 + a] = chh[a]; }
+    s_r[threadIdx.x >> 6][6] = ma;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      for (int a = 0; a < 3; ++a) { cl[a] = fminf(cl[a], s_r[w][a]); chh[a] = fmaxf(chh[a], s_r[w][3 + a]); }
+      ma = fmaxf(ma, s_r[w][6]);
+    }
     for (int a = 0; a < 3; ++a) { atomicMin(&root->cb_lo[a], f2o(cl[a])); atomicMax(&root->cb_hi[a], f2o(chh[a])); }
     atomicMax(&g->maxabs, __float_as_uint(ma));
   }
@@ -324,19 +354,13 @@ __global__ __launch_bounds__(64) void sah_split_kernel(const Task* __restrict__ 
   if (ti >= ntasks) return;
   const Task t = tasks[ti];
   const uint32_t* bins = tbins + (size_t)ti * 3 * NB * 7;
-  __shared__ float s_cost[3];
-  __shared__ int s_bin[3];
   const uint32_t n = t.end - t.begin;
   float ext[3];
   for (int a = 0; a < 3; ++a) ext[a] = o2f(t.cb_hi[a]) - o2f(t.cb_lo[a]);
-  if (threadIdx.x < 3) {
-    float c = __builtin_huge_valf();
-    int b = -1;
-    if (ext[threadIdx.x] > 0.0f) sweep_axis(bins + threadIdx.x * NB * 7, c, b);
-    s_cost[threadIdx.x] = c;
-    s_bin[threadIdx.x] = b;
-  }
-  __syncthreads();
+  const bool on[3] = {ext[0] > 0.0f, ext[1] > 0.0f, ext[2] > 0.0f};
+  float w_cost;
+  int w_axis, w_bin;
+  sweep_wave(bins, on, w_cost, w_axis, w_bin);
   if (threadIdx.x != 0) return;
   Split sp;
   sp.axis = -1; sp.bin = -1; sp.lo = 0.0f; sp.scale = 0.0f; sp.nleft = 0; sp.child_task[0] = sp.child_task[1] = -1;
@@ -349,9 +373,7 @@ __global__ __launch_bounds__(64) void sah_split_kernel(const Task* __restrict__ 
   int best_axis = -1, best_bin = -1;
   float best_cost = __builtin_huge_valf();
   const bool sah = ext[axis] > 0.0f && t.depth + need + 1 < max_depth;
-  if (sah)
-    for (int a = 0; a < 3; ++a)
-      if (s_bin[a] >= 0 && s_cost[a] < best_cost) { best_cost = s_cost[a]; best_axis = a; best_bin = s_bin[a]; }
+  if (sah) { best_cost = w_cost; best_axis = w_axis; best_bin = w_bin; }
   // the node's box: union of all bins of an axis with non-zero extent (every reference is binned there)
   const int ba = ext[0] > 0.0f ? 0 : (ext[1] > 0.0f ? 1 : 2);
   if (!sah || best_axis < 0 || ext[ba] <= 0.0f) {
@@ -485,8 +507,6 @@ __global__ __launch_bounds__(BT) void sah_subtree_kernel(RefBuf refs, RefBuf alt
   __shared__ uint32_t sb[3 * NB * 7];
   __shared__ float s_red[(BT / 64) * 12];
   __shared__ uint32_t s_scan[BT / 64];
-  __shared__ float s_cost[3];
-  __shared__ int s_bin[3];
   __shared__ int s_sp;
   __shared__ int s_act;  // 0 leaf, 1 SAH split, 2 balanced split
   __shared__ int s_axis, s_bbin;
@@ -557,19 +577,12 @@ __global__ __launch_bounds__(BT) void sah_subtree_kernel(RefBuf refs, RefBuf alt
         }
       }
       __syncthreads();
-      if (threadIdx.x < 3) {
-        float c = __builtin_huge_valf();
-        int b = -1;
-        if (ext[threadIdx.x] > 0.0f) sweep_axis(sb + threadIdx.x * NB * 7, c, b);
-        s_cost[threadIdx.x] = c;
-        s_bin[threadIdx.x] = b;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        int best_axis = -1, best_bin = -1;
-        float best_cost = __builtin_huge_valf();
-        for (int a = 0; a < 3; ++a)
-          if (s_bin[a] >= 0 && s_cost[a] < best_cost) { best_cost = s_cost[a]; best_axis = a; best_bin = s_bin[a]; }
+      if (threadIdx.x < 64) {
+        const bool on[3] = {ext[0] > 0.0f, ext[1] > 0.0f, ext[2] > 0.0f};
+        float best_cost;
+        int best_axis, best_bin;
+        sweep_wave(sb, on, best_cost, best_axis, best_bin);
+        if (threadIdx.x == 0) {
         s_act = 2;
         if (best_axis >= 0) {
           const float leaf_cost = box_area(ob) * (float)n;
@@ -586,6 +599,7 @@ __global__ __launch_bounds__(BT) void sah_subtree_kernel(RefBuf refs, RefBuf alt
             for (int k = 0; k <= best_bin; ++k) nl += sb[(best_axis * NB + k) * 7 + 6];
             s_nl = nl;
           }
+        }
         }
       }
     } else if (threadIdx.x == 0) {
