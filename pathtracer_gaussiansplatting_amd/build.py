@@ -20,7 +20,7 @@ INCLUDE = os.path.join(ROOT, "include")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libptgs.so")
 
-SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "bvh_sah_gpu.hip", "capture.cpp", "capture_io.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp",
+SOURCES = ["api.cpp", "bvh.cpp", "bvh_gpu.hip", "bvh_sah_gpu.hip", "bvh_collapse_gpu.hip", "capture.cpp", "capture_io.cpp", "comm.cpp", "jpeg.cpp", "scene.cpp", "textures.cpp",
            "pt_kernels.hip", "pt_wavefront.hip", "raster.hip", "splat.hip", "knn.hip", "gltf.cpp", "image_decode.cpp", "ply.cpp", "sampling.cpp"]
 # pure host code (scene ingest): plain g++, no device pass
 HOST_SOURCES = {"gltf.cpp", "image_decode.cpp", "ply.cpp", "sampling.cpp", "capture_io.cpp", "jpeg.cpp"}

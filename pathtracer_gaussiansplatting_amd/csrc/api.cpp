@@ -295,19 +295,21 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     float ms = 0.0f;
     hipError_t e = (c->flags & PTGS_FLAG_GPU_LBVH) ? build_bvh_gpu(tris, PTGS_STACK - 1, g, &ms)
                                                   : build_bvh_sah_gpu(tris, PTGS_BVH_LEAF, PTGS_STACK - 1, g, &ms);
-    if (e == hipSuccess) {  // 4-wide collapse on the host (D2H of the BVH2 nodes, collapse, H2D)
+    if (e == hipSuccess) {  // 4-wide collapse on the GPU (fan-out 4, else 3, else 2, as collapse_fit)
       auto t0 = std::chrono::steady_clock::now();
-      std::vector<float> n2((size_t)g.num_nodes * 16), n4;
-      uint32_t num4 = 0, dep4 = 0;
-      if ((e = hipMemcpy(n2.data(), g.nodes, n2.size() * 4, hipMemcpyDeviceToHost)) == hipSuccess) {
-        (void)hipFree(g.nodes);
-        g.nodes = nullptr;
-        if (!collapse_fit(n2, n4, num4, dep4) || hipMalloc(&g.nodes, n4.size() * 4) != hipSuccess ||
-            hipMemcpy(g.nodes, n4.data(), n4.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-          e = hipErrorNotSupported;
-        g.num_nodes = num4;
-        g.depth = dep4;
+      float4* n4 = nullptr;
+      uint32_t num4 = 0, need = 0, dep4 = 0;
+      for (int fan = 4; fan >= 2 && e == hipSuccess; --fan) {
+        (void)hipFree(n4);
+        n4 = nullptr;
+        e = collapse_bvh4_gpu(g.nodes, g.num_nodes, fan, &n4, &num4, &need, &dep4);
+        if (e == hipSuccess && need < PTGS_STACK) break;
       }
+      if (e == hipSuccess && need >= PTGS_STACK) e = hipErrorNotSupported;
+      (void)hipFree(g.nodes);
+      g.nodes = n4;
+      g.num_nodes = num4;
+      g.depth = dep4;
       auto t1 = std::chrono::steady_clock::now();
       ms += (float)std::chrono::duration<double, std::milli>(t1 - t0).count();  // build_ms includes it
     }

@@ -29,4 +29,9 @@ hipError_t build_bvh_gpu(const std::vector<BuildTri>& tris, uint32_t max_depth, 
 hipError_t build_bvh_sah_gpu(const std::vector<BuildTri>& tris, uint32_t max_leaf, uint32_t max_depth, GpuBvh& out,
                              float* build_ms);
 
+// The 4-wide collapse of a device BVH2 (collapse_bvh4 of bvh.h, same output word for word) on the
+// GPU: *nodes4 is a new device allocation of *num4 nodes (128 B each); max_stack / depth4 as there.
+hipError_t collapse_bvh4_gpu(const float4* nodes2, uint32_t num2, int max_children, float4** nodes4, uint32_t* num4,
+                             uint32_t* max_stack, uint32_t* depth4);
+
 }  // namespace ptgs
