@@ -500,6 +500,32 @@ def main():
         }
         del haccum, hdepth, hdg
 
+    # ------------------------------------------------------------------ C1: Cornell box, 256x256, 1 spp
+    # (BASELINE config 1, the reference's CPU-runnable case: here on the GPU, one launch per frame)
+    if not args.no_pt and world == 1:
+        from pathtracer_gaussiansplatting_amd import cornell_box_scene
+        c1 = cornell_box_scene()
+        c1.blue_noise = Y.blue_noise(1024)
+        r.upload_scene(c1)
+        c1pose = Camera(aspect=1.0).toroidal(218.6429, 21.5660, 3.5, 3.0)
+        c1acc = torch.zeros((256, 256, 4), dtype=torch.float32, device="cuda")
+        c1n = 50
+        for k in range(3):
+            r.trace_camera(make_ubo(c1pose, c1, k), 256, 256, c1acc, spp=1, stream=stream)
+        torch.cuda.synchronize()
+        r.stats_reset(stream)
+        t0 = time.perf_counter()
+        for k in range(c1n):
+            r.trace_camera(make_ubo(c1pose, c1, k), 256, 256, c1acc, spp=1, stream=stream)
+        torch.cuda.synchronize()
+        c1dt = (time.perf_counter() - t0) / c1n
+        c1st = r.stats()
+        out["c1"] = {"workload": "C1 Cornell box (rt-box of bunny_box.json), 256x256, 1 spp per frame",
+                     "ms_per_frame": round(c1dt * 1e3, 4),
+                     "mrays_per_s": round((c1st.extension_rays + c1st.shadow_rays) / c1n / c1dt / 1e6, 2),
+                     "note": "launch-bound: 65k pixels per frame"}
+        del c1acc
+
     # ------------------------------------------------------------------ C5 (opt-in): the 8-GPU config
     # 1M-tri atrium + 10M C2-distributed Gaussians in its camera frame, 3840x2160, 256 spp in total.
     # Rank g traces samples g, g+N, ... (256/N each, SUM), one all-reduce of the radiance (every rank
