@@ -6,8 +6,11 @@
 //   recordCommandBuffer's vkCmdTraceRaysKHR :1971-1976 + rt_output_image running mean
 //       -> ptgs_trace_camera
 //   torus trace :1893-1900 / :2787-2794 -> ptgs_trace_torus
+// Largest BVH leaf (triangles). C3 at 64 spp (tools/ab_pt.py, interleaved): 1 -> 3 602, 2 -> 4 849,
+// 3 -> 4 836, 4 -> 4 463, 8 -> -10% Mrays/s; 3 keeps the tree a level shallower than 2 for the
+// traversal-stack budget of large meshes
 #ifndef PTGS_BVH_LEAF
-#define PTGS_BVH_LEAF 4
+#define PTGS_BVH_LEAF 3
 #endif
 #include <hip/hip_runtime.h>
 

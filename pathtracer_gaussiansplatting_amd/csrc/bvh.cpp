@@ -9,6 +9,9 @@
 #ifndef PTGS_BVH_CT
 #define PTGS_BVH_CT 0.125f
 #endif
+#ifndef PTGS_BVH_BINS
+#define PTGS_BVH_BINS 32  // (bvh_sah_gpu.hip reproduces this builder with 32 bins)
+#endif
 
 namespace ptgs {
 
@@ -92,7 +95,7 @@ struct Builder {
     uint32_t need = 0;
     while (((uint64_t)max_leaf << need) < n) need++;
     if (ext[axis] > 0.0f && d + need + 1 < max_depth) {
-      const int NB = 32;
+      const int NB = PTGS_BVH_BINS;
       float best_cost = std::numeric_limits<float>::infinity();
       int best_axis = -1, best_bin = -1;
       for (int a = 0; a < 3; ++a) {

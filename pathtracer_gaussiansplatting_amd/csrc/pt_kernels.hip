@@ -13,6 +13,11 @@
 
 #include "pt_shade.h"
 #include "pt_launch.h"
+#include "xcd.h"
+
+#ifndef PTGS_PT_XCD_REMAP
+#define PTGS_PT_XCD_REMAP 0
+#endif
 
 namespace ptgs {
 
@@ -50,8 +55,15 @@ __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevSc
                                                         uint32_t mode, unsigned long long* counters) {
   const uint32_t lid = threadIdx.x;
   const uint32_t wave = lid >> 6, lane = lid & 63u;
-  const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-  const uint32_t y = row0 + blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+#if PTGS_PT_XCD_REMAP
+  // XCD-aware: the workgroups of one XCD trace one horizontal strip of 16x16 tiles (shared L2 nodes)
+  const uint32_t tl = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const uint32_t bx = tl % gridDim.x, by = tl / gridDim.x;
+#else
+  const uint32_t bx = blockIdx.x, by = blockIdx.y;
+#endif
+  const uint32_t x = bx * 16u + (wave & 1u) * 8u + (lane & 7u);
+  const uint32_t y = row0 + by * 16u + (wave >> 1) * 8u + (lane >> 3);
   const bool active = (x < W) && (y < row1);
 
   __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];

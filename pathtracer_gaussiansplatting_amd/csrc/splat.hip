@@ -25,10 +25,14 @@
 
 #include "../../include/ptgs/ptgs.h"
 #include "detmath.h"
+#include "xcd.h"
 #include "splat.h"
 
 namespace ptgs {
 
+#ifndef GS_XCD_REMAP
+#define GS_XCD_REMAP 0
+#endif
 #define GS_BLOCK_X 16
 #define GS_BLOCK_Y 16
 #define GS_BLOCK (GS_BLOCK_X * GS_BLOCK_Y)
@@ -857,7 +861,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   __shared__ uint8_t s_sslot[GS_BLOCK];  // small tiles: staging slot of sorted position p
   if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+#if GS_XCD_REMAP
+  // XCD-aware: the workgroups of one XCD blend one horizontal strip of tiles, so the records of the
+  // Gaussians they share stay in that XCD's L2
+  const uint32_t tl = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const uint32_t tile_x = tl % gridDim.x, tile_y = cam.row_begin + tl / gridDim.x;
+#else
   const uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
+#endif
   const uint32_t tile = tile_y * cam.grid_x + tile_x;
   const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
   // Stage a record as the quadratic in tile-local pixel coordinates (ux, uy):
