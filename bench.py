@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-hybrid", action="store_true")
     ap.add_argument("--no-gpu-bvh", action="store_true")
     ap.add_argument("--no-wavefront", action="store_true")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 Cornell-box leg")
     ap.add_argument("--no-gs-1m", action="store_true", help="skip the 1M-Gaussian splat and the point-cloud init legs")
     ap.add_argument("--no-gs-10m", action="store_true", help="skip the 10M-Gaussian 3840x2160 splat leg (C5's splat)")
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
@@ -502,7 +503,7 @@ def main():
 
     # ------------------------------------------------------------------ C1: Cornell box, 256x256, 1 spp
     # (BASELINE config 1, the reference's CPU-runnable case: here on the GPU, one launch per frame)
-    if not args.no_pt and world == 1:
+    if not args.no_pt and not args.no_c1 and world == 1:
         from pathtracer_gaussiansplatting_amd import cornell_box_scene
         c1 = cornell_box_scene()
         c1.blue_noise = Y.blue_noise(1024)
