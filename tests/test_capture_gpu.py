@@ -64,3 +64,53 @@ def test_capture_dataset(renderer, tmp_path):
     lines = open(os.path.join(out, "points3d.ply")).read().splitlines()
     nvalid = int(np.count_nonzero(hg["flag"] > 0))
     assert lines[2] == f"element vertex {nvalid}" and len(lines) == 13 + nvalid and nvalid > 100
+
+
+def test_capture_files_equal_oracle_pipeline(renderer, oracle_lib, tmp_path):
+    """ptgs_capture_dataset's output files against the same pipeline run on the CPU oracle: every view
+    traced by the oracle at the capture's pose (accumulation_steps samples, frame 0), sRGB8-encoded by
+    the oracle, every 2nd pixel of every 2nd row, through the JPEG writer: the JPEG files are equal
+    byte for byte; the point cloud (the oracle's torus HitData over the same frames, through the PLY
+    writer) too. (The writers are the library's host code in both cases: this pins trace, encode,
+    downscale, pose and accumulation order of the capture against the oracle.)"""
+    import ctypes as C
+    from pathtracer_gaussiansplatting_amd._abi import Ubo
+    sc = U.cornell()
+    renderer.upload_scene(sc)
+    W, H, n_views, steps, fov = 64, 48, 3, 2, 60.0
+    base = make_ubo(U.cornell_pose(W / H), sc, 0, height=H)
+    samples = Y.torus_samples(500)
+    ds = torch.from_numpy(samples.view(np.float32).copy()).cuda()
+    push = torus_push(major_radius=3.5, minor_radius=1.0, height=3.0)
+    out = str(tmp_path / "dataset")
+    capture.capture_dataset(renderer, base, out, W, H, samples=ds, num_samples=len(samples), torus_push=push,
+                            total_positions=n_views, accumulation_steps=steps, min_beta=-30.0, max_beta=30.0,
+                            fov_deg=fov)
+    ab = capture.capture_poses(n_views, 13, -30.0, 30.0)
+    for i in range(n_views):
+        pose = Camera(aspect=W / H, fov_deg=fov).toroidal(float(ab[i, 0]), float(ab[i, 1]), 3.5, 3.0)
+        u = Ubo()
+        C.memmove(C.addressof(u), C.addressof(base), C.sizeof(Ubo))  # capture.cpp: ubo = *d->ubo, then
+        u.view[:] = [float(x) for x in pose.view]                      # the pose, frame 0, fov, height
+        u.proj[:] = [float(x) for x in pose.proj]
+        u.camera_pos[:] = [float(x) for x in pose.position]
+        u.frame_count = 0
+        u.fov = float(np.float32(fov) * np.float32(0.01745329251994329576923690768489))
+        u.height = float(H)
+        acc = np.zeros((H, W, 4), np.float32)
+        oracle_lib.trace_camera(sc.desc(), u, W, H, acc, spp=steps)
+        px = oracle_lib.encode_srgb8(acc).view(np.uint8).reshape(H, W, 4)[::2, ::2].copy()
+        px[..., 3] = 255
+        ref = str(tmp_path / f"ref_{i}.jpg")
+        capture.write_jpeg(ref, np.ascontiguousarray(px))
+        got = open(os.path.join(out, "train", f"r_{i}.jpg"), "rb").read()
+        assert got == open(ref, "rb").read(), f"view {i}: JPEG bytes differ from the oracle pipeline's"
+    hits = np.zeros(len(samples), HITDATA_DTYPE)
+    for frame in range(steps):
+        uf = Ubo()
+        C.memmove(C.addressof(uf), C.addressof(base), C.sizeof(Ubo))
+        uf.frame_count = frame
+        oracle_lib.trace_torus(sc.desc(), uf, push, samples, hits)
+    ref_ply = str(tmp_path / "ref.ply")
+    capture.write_ply(ref_ply, hits)
+    assert open(os.path.join(out, "points3d.ply"), "rb").read() == open(ref_ply, "rb").read()

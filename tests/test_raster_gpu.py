@@ -180,8 +180,9 @@ def test_gaussians_stream_ordered_graph_replay(renderer, oracle_lib):
     del graph
 
 
-def test_gaussians_tile_row_shards_compose(renderer):
-    """§8e screen-tile shard: rendering tile rows [0,a) and [a,gy) separately == the full frame."""
+def test_gaussians_tile_row_shards_compose(renderer, oracle_lib):
+    """§8e screen-tile shard: rendering tile rows [0,a) and [a,gy) separately == the full frame, and
+    the composed shards against the oracle's frame (1e-4 relative L2)."""
     n, W, H = 5000, 200, 120
     g = Y.gaussians_c2(n, seed=3)
     ubo = _gauss_ubo(W, H)
@@ -194,6 +195,10 @@ def test_gaussians_tile_row_shards_compose(renderer):
     renderer.splat_gaussians(dg, ubo, W, H, part, tile_rows=(3, gy))
     torch.cuda.synchronize()
     assert torch.equal(full, part)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H)["image"]
+    got = part.cpu().numpy()
+    err = float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30))
+    assert err < 1e-4, err
 
 
 def test_torus_parity(renderer, oracle_lib):
