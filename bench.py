@@ -601,6 +601,23 @@ def main():
                       f"({cst.samples} samples, {cst.extension_rays + cst.shadow_rays} rays, {cdt:.1f} s, "
                       f"incl. oracle BVH build)",
         }
+        if "c1" in out:
+            # C1 (timed in full on the CPU): the Cornell frames of the GPU leg
+            from pathtracer_gaussiansplatting_amd import cornell_box_scene
+            c1 = cornell_box_scene()
+            c1.blue_noise = Y.blue_noise(1024)
+            c1pose = Camera(aspect=1.0).toroidal(218.6429, 21.5660, 3.5, 3.0)
+            c1acc = np.zeros((256, 256, 4), np.float32)
+            c1desc = c1.desc()
+            nfr, rays, t0 = 0, 0, time.perf_counter()
+            while nfr == 0 or time.perf_counter() - t0 < 2.0:
+                c1st = oracle.trace_camera(c1desc, make_ubo(c1pose, c1, nfr), 256, 256, c1acc, spp=1, threads=threads)
+                rays += c1st.extension_rays + c1st.shadow_rays
+                nfr += 1
+            c1dt = time.perf_counter() - t0
+            out["cpu_baseline"]["c1"] = {"value": round(rays / c1dt / 1e6, 4), "unit": "Mrays/s", "cores": threads,
+                                         "kind": "port", "sample": f"{nfr} full C1 frames (256x256, 1 spp), "
+                                                                   f"{c1dt / nfr * 1e3:.2f} ms each"}
         if not args.no_gs:
             # the oracle's 3DGS forward is OpenMP-threaded (preprocess, duplicate-with-keys, blend; the
             # pair sort is serial): OMP_NUM_THREADS threads, whole C2 frames for >= 3 s
