@@ -243,6 +243,9 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
 //           the ranges.
 // Order inside a tile's segment depends on LDS atomic order and is fixed by the blend's per-tile sort.
 #define GS_BIN_THREADS 1024
+#ifndef GS_COUNT_THREADS
+#define GS_COUNT_THREADS 1024  // the count's workgroup (the scatter keeps GS_BIN_THREADS)
+#endif
 #define GS_MAX_CHUNKS 256    // colscan: 4 waves x 64 chunks
 #ifndef GS_CHUNK_MIN
 #define GS_CHUNK_MIN 512     // Gaussians per chunk (at least)
@@ -312,6 +315,9 @@ __device__ __forceinline__ void gs_clip(const ushort4& rc, uint32_t ty0, uint32_
 // each wave first filters (64 rects per step, GS_WALK_PF steps in flight; ballot + mbcnt append the
 // hits to its GS_WQ-entry LDS ring) and expands 64 queued entries at a time (depths gathered then).
 #define GS_WQ 128
+#ifndef GS_SCATTER_DIRECT
+#define GS_SCATTER_DIRECT 1  // one band (1080p): direct walk, -0.4 us at C2 (kernel trace)
+#endif
 #define GS_WALK_PF 4
 template <typename F>
 __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* __restrict__ rects,
@@ -366,7 +372,7 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
 }
 
 // preprocess + count. Block (0, 0) also re-arms the frame's counters.
-__global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
+__global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                       uint32_t* __restrict__ hist,
                                                                       uint32_t* __restrict__ total,
                                                                       uint32_t* __restrict__ large_ctr,
@@ -375,7 +381,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam c
   uint32_t ty0, ty1;
   gs_band(bg, ty0, ty1);
   const uint32_t nt = (ty1 - ty0) * bg.grid_x;
-  for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) s_hist[k] = 0;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_COUNT_THREADS) s_hist[k] = 0;
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     total[1] = 0;  // largest tile (colscan's atomicMax; the scatter hands it to the host)
     large_ctr[0] = 0;  // large-tile list length (colscan)
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam c
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t b0 = blockIdx.y * bg.chunk, b1 = min(A.n, b0 + bg.chunk);
-  for (uint32_t base = b0 + wave * 64u; base < b1; base += GS_BIN_THREADS) {
+  for (uint32_t base = b0 + wave * 64u; base < b1; base += GS_COUNT_THREADS) {
     const uint32_t i = base + lane;
     ushort4 rc = make_ushort4(0, 0, 0, 0);
     if (i < b1) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i) : gs_preprocess_one<false>(cam, A, i);
@@ -398,29 +404,34 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_count_kernel(SplatCam c
   }
   __syncthreads();
   uint32_t* row = hist + (size_t)blockIdx.y * bg.tiles + ty0 * bg.grid_x;
-  for (uint32_t k = threadIdx.x; k < nt; k += GS_BIN_THREADS) row[k] = s_hist[k];
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_COUNT_THREADS) row[k] = s_hist[k];
 }
 
 // One 256-work-item block per 64-tile group g: wave w sums chunks [w*cpw, (w+1)*cpw) of the group's
 // 64 tiles (lane = tile: coalesced rows), then rewrites hist[c][t] as the exclusive prefix over c.
 // Outputs per tile (offset inside the group, total), per group its total, atomicMax of the largest
 // tile into total[1], and the tiles of more than `thr` pairs appended to the large-tile list.
-__global__ __launch_bounds__(256) void gs_bin_colscan_kernel(BinGrid bg, uint32_t* __restrict__ hist,
+#ifndef GS_COLSCAN_WAVES
+#define GS_COLSCAN_WAVES 16
+#endif
+#define GS_COLSCAN_THREADS (64 * GS_COLSCAN_WAVES)
+__global__ __launch_bounds__(GS_COLSCAN_THREADS) void gs_bin_colscan_kernel(BinGrid bg, uint32_t* __restrict__ hist,
                                                              uint2* __restrict__ tile_info,
                                                              uint32_t* __restrict__ group_total,
                                                              uint32_t* __restrict__ total, uint32_t thr,
                                                              uint32_t* __restrict__ large,
                                                              uint32_t* __restrict__ large_ctr) {
-  __shared__ uint32_t s_ws[4][64];
+  __shared__ uint32_t s_ws[GS_COLSCAN_WAVES][64];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t t = blockIdx.x * 64u + lane;
   const bool ok = t < bg.tiles;
-  const uint32_t cpw = (bg.chunks + 3u) / 4u, c0 = wave * cpw, c1 = min(bg.chunks, c0 + cpw);
+  const uint32_t cpw = (bg.chunks + GS_COLSCAN_WAVES - 1u) / GS_COLSCAN_WAVES, c0 = wave * cpw,
+                 c1 = min(bg.chunks, c0 + cpw);
   // all of this wave's rows in flight at once (cpw <= 64: registers, fully unrolled)
-  uint32_t h[GS_MAX_CHUNKS / 4];
+  uint32_t h[GS_MAX_CHUNKS / GS_COLSCAN_WAVES];
   uint32_t sum = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < GS_MAX_CHUNKS / 4; ++k) {
+  for (uint32_t k = 0; k < GS_MAX_CHUNKS / GS_COLSCAN_WAVES; ++k) {
     h[k] = (ok && c0 + k < c1) ? hist[(size_t)(c0 + k) * bg.tiles + t] : 0u;
     sum += h[k];
   }
@@ -429,13 +440,15 @@ __global__ __launch_bounds__(256) void gs_bin_colscan_kernel(BinGrid bg, uint32_
   uint32_t run = 0;
   for (uint32_t w = 0; w < wave; ++w) run += s_ws[w][lane];
 #pragma unroll
-  for (uint32_t k = 0; k < GS_MAX_CHUNKS / 4; ++k)
+  for (uint32_t k = 0; k < GS_MAX_CHUNKS / GS_COLSCAN_WAVES; ++k)
     if (ok && c0 + k < c1) {
       hist[(size_t)(c0 + k) * bg.tiles + t] = run;
       run += h[k];
     }
   if (wave != 0) return;
-  const uint32_t tot = s_ws[0][lane] + s_ws[1][lane] + s_ws[2][lane] + s_ws[3][lane];
+  uint32_t tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < GS_COLSCAN_WAVES; ++w) tot += s_ws[w][lane];
   const uint32_t incl = wave_incl_scan(tot);
   if (ok) tile_info[t] = make_uint2(incl - tot, tot);  // (offset inside the group, tile total)
   const bool big = ok && tot > thr;
@@ -514,7 +527,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
 #ifdef GS_PROBE_NO_WALK
   return;
 #endif
-  gs_walk_chunk(bg, rects, depths, n, ty0, ty1, s_q, [&](uint32_t i, uint32_t x, uint32_t y, float d) {
+  auto put = [&](uint32_t i, uint32_t x, uint32_t y, float d) {
     const unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | i;
     const uint32_t k = (y - ty0) * bg.grid_x + x;
     const uint32_t rel = atomicAdd(s_cur + k, 1u), dst = s_tot[k];
@@ -522,7 +535,26 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
       pairs[(dst & 0x7FFFFFFFu) + rel] = key;
     else
       tile_slots[dst + rel] = key;
-  });
+  };
+#if GS_SCATTER_DIRECT
+  if (bg.bands == 1) {  // one band: every rect meets it, so no filtering ring (one Gaussian per lane, as the count)
+    const uint32_t b0 = c * bg.chunk, b1 = min(n, b0 + bg.chunk);
+    for (uint32_t base = b0 + wv * 64u; base < b1; base += GS_BIN_THREADS) {
+      const uint32_t i = base + lane;
+      ushort4 rc = make_ushort4(0, 0, 0, 0);
+      float d = 0.0f;
+      if (i < b1) {
+        rc = rects[i];
+        d = depths[i];
+      }
+      uint32_t xw, yh;
+      gs_clip(rc, ty0, ty1, xw, yh);
+      if (__ballot(yh != 0u)) gs_expand<true>(lane, i, xw, yh, d, put);
+    }
+    return;
+  }
+#endif
+  gs_walk_chunk(bg, rects, depths, n, ty0, ty1, s_q, put);
 }
 
 // ascending bitonic sort ("flip" network: every comparator puts the min at the lower index) over
@@ -807,6 +839,11 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
 
 // ---- blend ----------------------------------------------------------------------------------------
 #define GS_ARENA (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)  // staged records + per-quadrant lists
+#ifndef GS_SMALL_RANK
+// small tiles of at most this many pairs are ranked by counting instead of sorted by the register
+// bitonic network: blend 70.6 -> 68.1 us at C2 (kernel trace; 128: 67.8, within noise)
+#define GS_SMALL_RANK 256
+#endif
 #define GS_MID 512  // tiles of (256, GS_MID] pairs are sorted inside the blend (rank counting)
 
 struct GStage {  // one staged blend record (see gs_preprocess_one)
@@ -818,10 +855,11 @@ struct GStage {  // one staged blend record (see gs_preprocess_one)
 // dispatcher's dynamic balancing, 103 vs 72 us at C2; a tile-pair workgroup shading two pixels per
 // lane in packed f32 measured 133 vs 104 us per frame: the per-pixel done / valid bookkeeping of the
 // pair and the strip lists cost more than the packing saved).
-//  sort     tiles of <= 256 pairs: in registers (one key per work-item; while the network runs, the
-//           blend records of the unsorted keys are already in flight, the key carries its staging
-//           slot in its low 8 bits), then publish the sorted keys (tile << 32 | depth) / values
-//           (gaussian). Larger tiles were sorted and published by gs_sort_large_kernel: their values
+//  sort     tiles of <= 256 pairs: one key per work-item, ranked by counting against all n keys in
+//           LDS (GS_SMALL_RANK; the register bitonic network remains for a smaller limit); while it
+//           runs, the blend records of the unsorted keys are already in flight, and the staging slot
+//           of sorted position r is recorded; then publish the sorted keys (tile << 32 | depth) /
+//           values (gaussian). Larger tiles were sorted and published by gs_sort_large_kernel: their values
 //           are streamed in batches of 256, the records of batch b + 1 (and the values of b + 2) in
 //           flight while batch b blends.
 //  blend    wave w shades the 8x8 quadrant q = w of the tile (x half w & 1, y half w >> 1), one pixel
@@ -904,7 +942,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   const bool mid = !small && n <= sorted_above;  // not sorted by gs_sort_large_kernel: sorted here
   const bool mid_lds = mid && n <= GS_MID;
   const unsigned long long tbits = (unsigned long long)tile << 32;
-  uint32_t my_slot = 0;  // small tiles: staging slot of sorted element tid
   float4 ra, rb, rc;     // records in flight: the unsorted keys' (small) / batch b + 1's (large)
   uint32_t g_next = 0;   // large tiles: gaussian of batch b + 2
   unsigned long long key = ~0ull;
@@ -921,6 +958,31 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     key = (k_cur & 0xFFFFFFFF00000000ull) | ((unsigned long long)g << 8) | tid;  // g < 2^24 (slot_keys)
   }
   if (small) {
+#if GS_SMALL_RANK
+   if (n <= GS_SMALL_RANK) {
+    // rank counting (keys are unique): every work-item of a wave holding keys counts the keys below
+    // its own over all n in LDS (uniform reads, two keys per read, no barrier in the loop) and
+    // records its staging slot at that rank
+    s_key[tid] = key;  // ~0 above n
+    __syncthreads();
+    uint32_t r = 0;
+    if (wave * 64u < n)
+      for (uint32_t j = 0; j < n; j += 2) {
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(s_key + j);
+        r += (uint32_t)(x.x < key) + (uint32_t)(x.y < key);
+      }
+    __syncthreads();  // every read of the keys is done before records overwrite them
+    if (tid < n) {
+      s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
+      if (keys_out) {
+        keys_out[range.x + r] = tbits | (key >> 32);
+        vals_out[range.x + r] = (uint32_t)(key >> 8) & 0xFFFFFFu;
+      }
+      s_sslot[r] = (uint8_t)tid;
+    }
+   } else
+#endif
+   {
     // bitonic network, one key per work-item: shuffles for strides < 64, LDS for 64 / 128
     uint32_t npad = 1;
     while (npad < n) npad <<= 1;
@@ -952,9 +1014,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         keys_out[range.x + tid] = tbits | (key >> 32);
         vals_out[range.x + tid] = (uint32_t)(key >> 8) & 0xFFFFFFu;
       }
-      my_slot = (uint32_t)key & 0xFFu;
-      s_sslot[tid] = (uint8_t)my_slot;
+      s_sslot[tid] = (uint8_t)(key & 0xFFu);
     }
+   }
   } else {
     if (mid) {
       unsigned long long* seg = n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
@@ -1238,11 +1300,11 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   pa.rec = (float4*)w->rec.p;
   if ((e = mark(0))) return e;
   // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
-  hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS), band_lds, s, cam, pa,
+  hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_COUNT_THREADS), band_lds, s, cam, pa,
                      bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev);
   if ((e = hipGetLastError())) return e;
   if ((e = mark(1))) return e;
-  hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(256), 0, s, bgrid, (uint32_t*)w->hist.p,
+  hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(GS_COLSCAN_THREADS), 0, s, bgrid, (uint32_t*)w->hist.p,
                      (uint2*)w->tile_info.p, (uint32_t*)w->group_total.p, (uint32_t*)w->total.p, (uint32_t)GS_MID,
                      (uint32_t*)w->large.p, (uint32_t*)w->large_ctr.p);
   if ((e = hipGetLastError())) return e;
