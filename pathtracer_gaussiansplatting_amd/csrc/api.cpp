@@ -52,16 +52,19 @@ struct ptgs_ctx {
 
 namespace {
 
-// 4-wide collapse whose worst-case traversal stack fits PTGS_STACK: fan-out 4, else 3, else 2 (a
-// 2-wide "collapse" needs the BVH2 depth, which the builders keep below PTGS_STACK)
-static bool collapse_fit(const std::vector<float>& n2, std::vector<float>& n4, uint32_t& num4, uint32_t& dep4) {
-  for (int fan = 4; fan >= 2; --fan) {
-    uint32_t need = 0;
-    ptgs::collapse_bvh4(n2, n4, num4, need, dep4, fan);
-    if (need < PTGS_STACK) return true;
-  }
-  return false;
+// 4-wide collapse whose worst-case traversal stack fits PTGS_STACK with fan-out `fan` (a 2-wide
+// "collapse" needs the BVH2 depth, which the builders keep below PTGS_STACK)
+static bool collapse_fit(const std::vector<float>& n2, std::vector<float>& n4, uint32_t& num4, uint32_t& dep4, int fan) {
+  uint32_t need = 0;
+  ptgs::collapse_bvh4(n2, n4, num4, need, dep4, fan);
+  return need < PTGS_STACK;
 }
+
+// (leaf size, fan-out) tried in this order until the tree's worst-case stack need fits PTGS_STACK:
+// a large scene whose 3-triangle-leaf tree is too deep for a 4-wide collapse is rebuilt with 4-triangle
+// leaves before the fan-out is narrowed (C5's 1M-triangle atrium: a 2-wide fallback traced at 1.38
+// Grays/s, the 4-triangle-leaf 4-wide tree at ~2.1)
+static const int kBvhTries[][2] = {{PTGS_BVH_LEAF, 4}, {PTGS_BVH_LEAF + 1, 4}, {PTGS_BVH_LEAF, 3}, {PTGS_BVH_LEAF, 2}};
 
 int fail(ptgs_ctx* c, int code, const char* fmt, ...) {
   char buf[512];
@@ -296,25 +299,45 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
   if ((c->flags & PTGS_FLAG_GPU_BVH) && tris.size() >= 16) {
     GpuBvh g;
     float ms = 0.0f;
-    hipError_t e = (c->flags & PTGS_FLAG_GPU_LBVH) ? build_bvh_gpu(tris, PTGS_STACK - 1, g, &ms)
-                                                  : build_bvh_sah_gpu(tris, PTGS_BVH_LEAF, PTGS_STACK - 1, g, &ms);
-    if (e == hipSuccess) {  // 4-wide collapse on the GPU (fan-out 4, else 3, else 2, as collapse_fit)
-      auto t0 = std::chrono::steady_clock::now();
-      float4* n4 = nullptr;
-      uint32_t num4 = 0, need = 0, dep4 = 0;
-      for (int fan = 4; fan >= 2 && e == hipSuccess; --fan) {
-        (void)hipFree(n4);
-        n4 = nullptr;
-        e = collapse_bvh4_gpu(g.nodes, g.num_nodes, fan, &n4, &num4, &need, &dep4);
-        if (e == hipSuccess && need < PTGS_STACK) break;
+    hipError_t e = hipSuccess;
+    // (leaf, fan) as the host path (kBvhTries); the LBVH has fixed leaves: fan-out 4, 3, 2
+    const bool lbvh = (c->flags & PTGS_FLAG_GPU_LBVH) != 0;
+    const int tries = lbvh ? 3 : (int)(sizeof(kBvhTries) / sizeof(kBvhTries[0]));
+    int built_leaf = -1;
+    float4* n4 = nullptr;
+    uint32_t num4 = 0, need = PTGS_STACK, dep4 = 0;
+    for (int k = 0; k < tries; ++k) {
+      const int leaf = lbvh ? 0 : kBvhTries[k][0], fan = lbvh ? 4 - k : kBvhTries[k][1];
+      if (leaf != built_leaf) {  // (re)build the BVH2
+        if (built_leaf >= 0) {
+          (void)hipFree(g.nodes);
+          (void)hipFree(g.tris);
+          (void)hipFree(g.tri_flags);
+          g = GpuBvh{};
+        }
+        float bms = 0.0f;
+        e = lbvh ? build_bvh_gpu(tris, PTGS_STACK - 1, g, &bms) : build_bvh_sah_gpu(tris, leaf, PTGS_STACK - 1, g, &bms);
+        ms += bms;
+        if (e != hipSuccess) break;
+        built_leaf = leaf;
       }
-      if (e == hipSuccess && need >= PTGS_STACK) e = hipErrorNotSupported;
+      // 4-wide collapse on the GPU
+      auto t0 = std::chrono::steady_clock::now();
+      (void)hipFree(n4);
+      n4 = nullptr;
+      e = collapse_bvh4_gpu(g.nodes, g.num_nodes, fan, &n4, &num4, &need, &dep4);
+      auto t1 = std::chrono::steady_clock::now();
+      ms += (float)std::chrono::duration<double, std::milli>(t1 - t0).count();  // build_ms includes it
+      if (e != hipSuccess || need < PTGS_STACK) break;
+    }
+    if (e == hipSuccess && need >= PTGS_STACK) e = hipErrorNotSupported;
+    if (e == hipSuccess || e == hipErrorNotSupported) {
       (void)hipFree(g.nodes);
       g.nodes = n4;
       g.num_nodes = num4;
       g.depth = dep4;
-      auto t1 = std::chrono::steady_clock::now();
-      ms += (float)std::chrono::duration<double, std::milli>(t1 - t0).count();  // build_ms includes it
+    } else {
+      (void)hipFree(n4);
     }
     if (e == hipSuccess) {
       for (void* p : {(void*)g.nodes, (void*)g.tris, (void*)g.tri_flags}) c->scene_allocs.push_back(p);
@@ -332,24 +355,32 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
       (void)hipFree(g.tris);
       (void)hipFree(g.tri_flags);
     } else {
+      (void)hipFree(g.nodes);
+      (void)hipFree(g.tris);
+      (void)hipFree(g.tri_flags);
       return fail(c, PTGS_EHIP, "GPU BVH build: %s", hipGetErrorString(e));
     }
   }
   if (!built) {
     auto t0 = std::chrono::steady_clock::now();
     BvhOut bvh;
-    build_bvh(tris, PTGS_BVH_LEAF, PTGS_STACK - 1, bvh);
-    auto t1 = std::chrono::steady_clock::now();
-    if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
-    {
-      std::vector<float> n4;
-      uint32_t num4 = 0, dep4 = 0;
-      if (!collapse_fit(bvh.nodes, n4, num4, dep4))
-        return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
-      if ((rc = upload(c, (const float4*)n4.data(), n4.size() / 4, &s.nodes))) return rc;
-      bvh.num_nodes = num4;
-      bvh.depth = dep4;
+    std::vector<float> n4;
+    uint32_t num4 = 0, dep4 = 0;
+    int built_leaf = -1;
+    bool fits = false;
+    for (const auto& tr : kBvhTries) {
+      if (tr[0] != built_leaf) {
+        build_bvh(tris, tr[0], PTGS_STACK - 1, bvh);
+        built_leaf = tr[0];
+        if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
+      }
+      if ((fits = collapse_fit(bvh.nodes, n4, num4, dep4, tr[1]))) break;
     }
+    auto t1 = std::chrono::steady_clock::now();
+    if (!fits) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
+    if ((rc = upload(c, (const float4*)n4.data(), n4.size() / 4, &s.nodes))) return rc;
+    bvh.num_nodes = num4;
+    bvh.depth = dep4;
     if ((rc = upload(c, (const float4*)bvh.tris.data(), bvh.tris.size() / 4, &s.tris))) return rc;
     if ((rc = upload(c, bvh.tri_flags.data(), bvh.tri_flags.size(), &s.tri_flags))) return rc;
     c->info.num_bvh_nodes = bvh.num_nodes;

@@ -73,9 +73,10 @@ struct TraversalCounters {
 // of a workgroup (entry k of lane t at [k * 256 + t]: conflict-free ds_read/ds_write_b32).
 // 39 x 256 x 4 B = 39 KiB per workgroup (+ 1 KiB of slot rings in the wavefront kernels: 4
 // workgroups = 16 waves per CU fill the 160 KiB LDS). A 4-wide node pushes up to 3 entries: the
-// collapse (api.cpp) caps the fan-out until the tree's worst-case stack need fits (4-wide, else 3-,
-// else 2-wide, which the builder's depth bound fits). Needs measured: C3's 250k-triangle atrium 34,
-// C5's 1M-triangle atrium 38.
+// scene upload (api.cpp kBvhTries) rebuilds with 4-triangle leaves, then caps the fan-out, until the
+// tree's worst-case stack need fits (4-wide, else 3-, else 2-wide, which the builder's depth bound
+// fits). C3's 250k-triangle atrium fits with 3-triangle leaves; C5's 1M-triangle atrium takes the
+// 4-triangle-leaf 4-wide tree.
 #ifndef PTGS_STACK
 #define PTGS_STACK 39
 #endif
