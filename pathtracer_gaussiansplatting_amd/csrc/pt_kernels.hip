@@ -41,9 +41,11 @@ __device__ __forceinline__ void flush_counters(unsigned long long* counters, uin
   }
 }
 
-// 4 waves per SIMD (<= 128 VGPRs). With the NEE shadow ray traced after shading (resolve_shadow)
-// the kernel fits without scratch; round 1 held the shading state across the shadow traversal and
-// spilled 164 B per lane.
+// 4 waves per SIMD (<= 128 VGPRs; the 39-entry LDS stack allows no more workgroups anyway). With the
+// NEE shadow ray traced after shading (resolve_shadow) the timed instantiation keeps 96 B per lane of
+// scratch (spills in the shading code, once per bounce); round 1 held the shading state across the
+// shadow traversal and spilled 164 B per lane. PTGS_PT_MIN_WAVES=3 compiles without scratch and
+// measured 9% slower.
 #ifndef PTGS_PT_MIN_WAVES
 #define PTGS_PT_MIN_WAVES 4
 #endif
