@@ -93,6 +93,48 @@ def test_gaussians_large_tile_sorts(renderer, oracle_lib, n, W, H):
         assert err < 1e-4, (frame, err)
 
 
+def test_gaussians_tile_size_boundaries(renderer, oracle_lib):
+    """One tile per pair count around every sort path's limit (rank counting in the blend up to 256 and
+    up to 512, the radix kernel above, wave multiples of 64), tiny Gaussians at the tile centres on
+    seven depth levels (many equal-depth ties): sorted keys / values / ranges bit-exact, image < 1e-4,
+    on the first frame after a small one (in-blend sorts) and on the next two (radix kernel)."""
+    counts = [0, 1, 2, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1030]
+    W, H = 16 * len(counts), 16
+    ubo = _gauss_ubo(W, H)
+    proj = np.array(ubo.proj, np.float64)
+    rng = np.random.default_rng(17)
+    means = []
+    for t, c in enumerate(counts):
+        ndc_x = (2.0 * (16 * t + 7.5) + 1.0) / W - 1.0
+        ndc_y = (2.0 * 7.5 + 1.0) / H - 1.0
+        for i in range(c):
+            d = 4.0 + 0.5 * (i % 7)
+            means.append((ndc_x * d / proj[0], ndc_y * d / proj[5], -d))
+    n = len(means)
+    g = {"means": np.array(means, np.float32),
+         "scales": np.full((n, 3), 3e-4, np.float32),
+         "rotations": rng.normal(size=(n, 4)).astype(np.float32),
+         "opacities": rng.uniform(0.05, 0.95, n).astype(np.float32),
+         "colors": rng.uniform(0.0, 1.0, (n, 3)).astype(np.float32)}
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H)
+    per_tile = np.diff(ref["ranges"].reshape(-1, 2), axis=1).ravel()
+    np.testing.assert_array_equal(per_tile, counts)  # the construction puts each count in its own tile
+    dg = {k: _dev(v) for k, v in g.items()}
+    tiny = {k: _dev(v) for k, v in Y.gaussians_c2(10, seed=1).items()}
+    renderer.splat_gaussians(tiny, ubo, W, H, torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"))
+    for frame in range(3):
+        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        st = renderer.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
+        torch.cuda.synchronize()
+        b = renderer.splat_buffers()
+        assert st.num_rendered == ref["K"] == sum(counts)
+        np.testing.assert_array_equal(_read(renderer, b.sorted_keys, ref["K"], np.uint64), ref["keys"])
+        np.testing.assert_array_equal(_read(renderer, b.sorted_values, ref["K"], np.uint32), ref["vals"])
+        np.testing.assert_array_equal(_read(renderer, b.tile_ranges, 2 * b.num_tiles, np.uint32), ref["ranges"])
+        err = U.rel_l2(out.cpu().numpy(), ref["image"])
+        assert err < 1e-4, (frame, err)
+
+
 def test_gaussians_beyond_24bit_indices(renderer, oracle_lib):
     """2^24 + 3 Gaussians (the register sort packs the gaussian index in 24 bits): every tile goes
     through the LDS rank-count / radix sorts instead; 3000 visible, the rest behind the camera."""
