@@ -25,7 +25,7 @@
  * add/sub/mul/div/sqrt, no FMA contraction (-ffp-contract=off), fixed evaluation order of the GLSL
  * built-ins, and the polynomial sin/cos/exp2/log2 below. Ray/triangle intersection is
  * Moller-Trumbore with the closest-hit tie broken towards the lower triangle id, which makes the
- * hit independent of the acceleration structure (this file uses its own median-split BVH).
+ * hit independent of the acceleration structure (this file uses its own SAH BVH2).
  */
 #include <math.h>
 #include <stdint.h>
@@ -223,7 +223,7 @@ void oracle_camera_toroidal(float alpha_deg, float beta_deg, float radius, float
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* scene + BVH (oracle's own: median split, leaves <= 4)                                       */
+/* scene + BVH (oracle's own: binned SAH, median split on degenerate centroids, leaves <= 4)      */
 /* ------------------------------------------------------------------------------------------ */
 typedef struct {
     float lo[3], hi[3];
@@ -411,6 +411,82 @@ static int cmp_tri(const void* a, const void* b) {
     return (x->gid < y->gid) ? -1 : (x->gid > y->gid);
 }
 
+/* Binned SAH split of tris[first, first + count) (16 bins on the centroid axis of largest extent...
+ * all three axes tried); returns the left count, or 0 when no bin boundary separates the centroids.
+ * The oracle's tree only decides which boxes are tested: the closest hit is the minimum over
+ * (t, gid) of every candidate and any-hit is a boolean, so any valid tree gives the same image; a
+ * SAH tree with nearest-child-first traversal keeps the CPU baseline honest (bench.py). */
+#define OR_SAH_BINS 16
+static int sah_partition(OScene* s, int first, int count) {
+    float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = first; i < first + count; ++i) {
+        float lo[3], hi[3];
+        tri_bounds(&s->tris[i], lo, hi);
+        for (int a = 0; a < 3; ++a) { float c = lo[a] + hi[a]; clo[a] = mn(clo[a], c); chi[a] = mx(chi[a], c); }
+    }
+    float best = INFINITY;
+    int best_axis = -1, best_bin = -1;
+    for (int a = 0; a < 3; ++a) {
+        float ext = chi[a] - clo[a];
+        if (!(ext > 0.0f)) continue;
+        float blo[OR_SAH_BINS][3], bhi[OR_SAH_BINS][3];
+        int cnt[OR_SAH_BINS];
+        for (int k = 0; k < OR_SAH_BINS; ++k) {
+            cnt[k] = 0;
+            for (int q = 0; q < 3; ++q) { blo[k][q] = INFINITY; bhi[k][q] = -INFINITY; }
+        }
+        float scale = (float)OR_SAH_BINS / ext;
+        for (int i = first; i < first + count; ++i) {
+            float lo[3], hi[3];
+            tri_bounds(&s->tris[i], lo, hi);
+            int k = (int)((lo[a] + hi[a] - clo[a]) * scale);
+            k = k < 0 ? 0 : (k >= OR_SAH_BINS ? OR_SAH_BINS - 1 : k);
+            cnt[k]++;
+            for (int q = 0; q < 3; ++q) { blo[k][q] = mn(blo[k][q], lo[q]); bhi[k][q] = mx(bhi[k][q], hi[q]); }
+        }
+        float rarea[OR_SAH_BINS];
+        int rcnt[OR_SAH_BINS];
+        float alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int c = 0;
+        for (int k = OR_SAH_BINS - 1; k > 0; --k) {
+            for (int q = 0; q < 3; ++q) { alo[q] = mn(alo[q], blo[k][q]); ahi[q] = mx(ahi[q], bhi[k][q]); }
+            c += cnt[k];
+            float dx = ahi[0] - alo[0], dy = ahi[1] - alo[1], dz = ahi[2] - alo[2];
+            rarea[k] = c ? dx * dy + dy * dz + dz * dx : 0.0f;
+            rcnt[k] = c;
+        }
+        for (int q = 0; q < 3; ++q) { alo[q] = INFINITY; ahi[q] = -INFINITY; }
+        c = 0;
+        for (int k = 0; k < OR_SAH_BINS - 1; ++k) {
+            for (int q = 0; q < 3; ++q) { alo[q] = mn(alo[q], blo[k][q]); ahi[q] = mx(ahi[q], bhi[k][q]); }
+            c += cnt[k];
+            if (c == 0 || rcnt[k + 1] == 0) continue;
+            float dx = ahi[0] - alo[0], dy = ahi[1] - alo[1], dz = ahi[2] - alo[2];
+            float cost = (dx * dy + dy * dz + dz * dx) * (float)c + rarea[k + 1] * (float)rcnt[k + 1];
+            if (cost < best) { best = cost; best_axis = a; best_bin = k; }
+        }
+    }
+    if (best_axis < 0) return 0;
+    /* stable partition (deterministic tree) */
+    OTri* tmp = (OTri*)malloc(sizeof(OTri) * (size_t)count);
+    float scale = (float)OR_SAH_BINS / (chi[best_axis] - clo[best_axis]);
+    int nl = 0, nr = 0;
+    for (int pass = 0; pass < 2; ++pass)
+        for (int i = first; i < first + count; ++i) {
+            float lo[3], hi[3];
+            tri_bounds(&s->tris[i], lo, hi);
+            int k = (int)((lo[best_axis] + hi[best_axis] - clo[best_axis]) * scale);
+            k = k < 0 ? 0 : (k >= OR_SAH_BINS ? OR_SAH_BINS - 1 : k);
+            if ((k <= best_bin) == (pass == 0)) tmp[pass == 0 ? nl++ : count - 1 - nr++] = s->tris[i];
+        }
+    for (int i = 0; i < nr / 2; ++i) {  /* the right part was filled from the end: restore its order */
+        OTri t = tmp[nl + i]; tmp[nl + i] = tmp[count - 1 - i]; tmp[count - 1 - i] = t;
+    }
+    memcpy(s->tris + first, tmp, sizeof(OTri) * (size_t)count);
+    free(tmp);
+    return (nl > 0 && nr > 0) ? nl : 0;
+}
+
 static int build_node(OScene* s, int first, int count) {
     if (s->nnodes == s->cap) { s->cap = s->cap * 2 + 16; s->nodes = (ONode*)realloc(s->nodes, sizeof(ONode) * s->cap); }
     int idx = s->nnodes++;
@@ -428,13 +504,16 @@ static int build_node(OScene* s, int first, int count) {
     n.first = first;
     n.count = count;
     if (count > 4) {
-        int axis = 0;
-        float e0 = n.hi[0] - n.lo[0], e1 = n.hi[1] - n.lo[1], e2 = n.hi[2] - n.lo[2];
-        if (e1 > e0 && e1 >= e2) axis = 1;
-        else if (e2 > e0 && e2 > e1) axis = 2;
-        g_axis = axis;
-        qsort(s->tris + first, (size_t)count, sizeof(OTri), cmp_tri);
-        int half = count / 2;
+        int half = sah_partition(s, first, count);
+        if (half == 0) {  /* degenerate centroids: median split along the widest axis */
+            int axis = 0;
+            float e0 = n.hi[0] - n.lo[0], e1 = n.hi[1] - n.lo[1], e2 = n.hi[2] - n.lo[2];
+            if (e1 > e0 && e1 >= e2) axis = 1;
+            else if (e2 > e0 && e2 > e1) axis = 2;
+            g_axis = axis;
+            qsort(s->tris + first, (size_t)count, sizeof(OTri), cmp_tri);
+            half = count / 2;
+        }
         int l = build_node(s, first, half);
         int r = build_node(s, first + half, count - half);
         n.left = l;
@@ -564,9 +643,21 @@ static int or_anyhit_accept(const OScene* s, const OTri* t, float u, float v, ui
     return !(or_rnd(&h) > alpha);
 }
 
+/* entry distance of the ray into n's box within [tmin, tcap], or +inf (box_hit's test) */
+static float box_enter(const ORay* r, const ONode* n, float tcap) {
+    float tn = r->tmin, tf = tcap;
+    float o[3] = {r->o.x, r->o.y, r->o.z}, iv[3] = {r->inv.x, r->inv.y, r->inv.z};
+    for (int a = 0; a < 3; ++a) {
+        float t0 = (n->lo[a] - o[a]) * iv[a], t1 = (n->hi[a] - o[a]) * iv[a];
+        tn = mx(tn, mn(t0, t1));
+        tf = mn(tf, mx(t0, t1));
+    }
+    return tn <= tf * 1.0000004f ? tn : INFINITY;
+}
+
+/* n's box is hit; children nearest first, the farther one re-tested against the shortened h->t */
 static void closest(const OScene* s, const ONode* n, const ORay* r, OHit* h, uint32_t seed, uint64_t* nodes_visited) {
     (*nodes_visited)++;
-    if (!box_hit(r, n, h->t)) return;
     if (n->left < 0) {
         for (int i = n->first; i < n->first + n->count; ++i) {
             const OTri* t = &s->tris[i];
@@ -579,8 +670,11 @@ static void closest(const OScene* s, const ONode* n, const ORay* r, OHit* h, uin
         }
         return;
     }
-    closest(s, &s->nodes[n->left], r, h, seed, nodes_visited);
-    closest(s, &s->nodes[n->right], r, h, seed, nodes_visited);
+    const ONode *a = &s->nodes[n->left], *b = &s->nodes[n->right];
+    float ta = box_enter(r, a, h->t), tb = box_enter(r, b, h->t);
+    if (tb < ta) { const ONode* x = a; a = b; b = x; float y = ta; ta = tb; tb = y; }
+    if (ta != INFINITY) closest(s, a, r, h, seed, nodes_visited);
+    if (tb != INFINITY && box_hit(r, b, h->t)) closest(s, b, r, h, seed, nodes_visited);
 }
 
 static int anyhit(const OScene* s, const ONode* n, const ORay* r, uint32_t seed) {
@@ -602,7 +696,7 @@ static int anyhit(const OScene* s, const ONode* n, const ORay* r, uint32_t seed)
 static OHit trace_closest(const OScene* s, const ORay* r, uint32_t seed) {
     OHit h; h.t = r->tmax; h.u = 0; h.v = 0; h.gid = 0xffffffffu; h.tri = NULL;
     uint64_t dummy = 0;
-    if (s->ntris) closest(s, &s->nodes[0], r, &h, seed, &dummy);
+    if (s->ntris && box_hit(r, &s->nodes[0], h.t)) closest(s, &s->nodes[0], r, &h, seed, &dummy);
     return h;
 }
 
