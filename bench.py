@@ -592,7 +592,7 @@ def main():
         import oracle
         oracle.build()
         threads = min(16, os.cpu_count() or 1)
-        row_stride, spp_cpu = 1, 16  # ~10-30 s of CPU work on the box
+        row_stride, spp_cpu = 1, 64  # the whole C3 frame (every row, 64 spp): ~20 s of CPU work on the box
         acc = np.zeros((H, W, 4), np.float32)
         desc = scene.desc()
         cubo = make_ubo(pose, scene, 0, ambient=(0.3, 0.4, 0.5, 1.0), height=H)
