@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-gpu-bvh", action="store_true")
     ap.add_argument("--no-wavefront", action="store_true")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 Cornell-box leg")
+    ap.add_argument("--no-torus", action="store_true", help="skip the torus data-collection leg (SURVEY 8f #1)")
     ap.add_argument("--no-gs-1m", action="store_true", help="skip the 1M-Gaussian splat and the point-cloud init legs")
     ap.add_argument("--no-gs-10m", action="store_true", help="skip the 10M-Gaussian 3840x2160 splat leg (C5's splat)")
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
@@ -528,6 +529,36 @@ def main():
                      "mrays_per_s": round((c1st.extension_rays + c1st.shadow_rays) / c1n / c1dt / 1e6, 2),
                      "note": "launch-bound: 65k pixels per frame"}
         del c1acc
+
+    # ------------------------------------------------------------------ torus data collection
+    # rt_datacollect: 1M RaySamples (the reference's RANDOM generator, Morton-sorted) shot from the
+    # torus around the C1 Cornell box, 16 accumulation frames into the HitData running mean
+    if not args.no_pt and not args.no_torus and world == 1:
+        from pathtracer_gaussiansplatting_amd import HITDATA_DTYPE, cornell_box_scene, torus_push
+        tsc = cornell_box_scene()
+        tsc.blue_noise = Y.blue_noise(1024)
+        r.upload_scene(tsc)
+        tn = 1 << 20
+        tsamp = torch.from_numpy(np.ascontiguousarray(Y.torus_samples(tn)).view(np.float32)).cuda()
+        thits = torch.zeros(tn * (HITDATA_DTYPE.itemsize // 4), dtype=torch.float32, device="cuda")
+        tpush = torus_push(major_radius=3.5, minor_radius=1.0, height=3.0)
+        tpose = Camera(aspect=1.0).toroidal(218.6429, 21.5660, 3.5, 3.0)
+        tframes = 16
+        for k in range(2):
+            r.trace_torus(make_ubo(tpose, tsc, k), tpush, tsamp, tn, thits, stream=stream)
+        torch.cuda.synchronize()
+        r.stats_reset(stream)
+        t0 = time.perf_counter()
+        for k in range(tframes):
+            r.trace_torus(make_ubo(tpose, tsc, k), tpush, tsamp, tn, thits, stream=stream)
+        torch.cuda.synchronize()
+        tdt = time.perf_counter() - t0
+        tst = r.stats()
+        out["torus"] = {"workload": f"torus data collection: {tn} RaySamples (RANDOM, Morton-sorted) x {tframes} "
+                                    "accumulation frames, C1 Cornell box", "ms_per_frame": round(tdt / tframes * 1e3, 4),
+                        "mrays_per_s": round((tst.extension_rays + tst.shadow_rays) / tdt / 1e6, 1),
+                        "msamples_per_s": round(tn * tframes / tdt / 1e6, 1)}
+        del tsamp, thits
 
     # ------------------------------------------------------------------ C5: the 8-GPU config
     # 1M-tri atrium + 10M C2-distributed Gaussians in its camera frame, 3840x2160, 256 spp in total.

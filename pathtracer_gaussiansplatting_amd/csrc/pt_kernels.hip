@@ -141,8 +141,15 @@ __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevSc
   flush_counters(counters, ext_rays, c.shadow_rays, samples, tc, STATS);
 }
 
+// Untextured: 4 waves per SIMD (the LDS stack's limit) — the single trace / shade site fits 128 VGPRs
+// without scratch (the former first-ray + bounce-loop pair of sites needed 143; same speed on the
+// Cornell box's 1M-sample collection, tools/torus_ab.py: 0.62 ms per frame, 6.1 Grays/s). Textured:
+// no bound (at 128 VGPRs the texture fetches would spill 96 B per lane).
+#ifndef PTGS_TORUS_MIN_WAVES
+#define PTGS_TORUS_MIN_WAVES 4
+#endif
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp, TorusParams tp,
+__global__ __launch_bounds__(256, TEX ? 1 : PTGS_TORUS_MIN_WAVES) void pt_torus_kernel(DevScene sc, CamParams cp, TorusParams tp,
                                                        const ptgs_ray_sample* __restrict__ samples,
                                                        uint32_t n, uint32_t side, uint32_t frame,
                                                        ptgs_hitdata* __restrict__ hits,
@@ -181,23 +188,13 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
     p.hit_flag = 0.0f;
     p.color = mk3(0.0f); p.weight = mk3(1.0f); p.next_o = so; p.next_d = rd;
     p.hit_pos = mk3(0.0f); p.normal = mk3(0.0f, 1.0f, 0.0f);
-
-    Ray ray = make_ray(so, rd, 0.0f, 10000.0f);
-    ext_rays++;
-    Hit h = trace_closest<STATS, TEX>(sc, ray, p.seed, c.stack, tc);
-    if (STATS && h.gid != 0xffffffffu) tc.hits++;
-    ShadowQuery q;
-    q.flags = 0;
-    if (h.gid == 0xffffffffu) miss<true>(cp, p);
-    else closest_hit<true, TEX>(c, p, ray, h, q);
-    resolve_shadow<STATS, TEX>(c, p.color, p.seed, q, tc);
-
-    v3 fpos = p.hit_pos;
-    float fflag = p.hit_flag;
-    v3 fnorm = p.normal;
-    if (p.hit_flag > 0.5f) {
-      acc = acc + p.color * thr;
-      for (int depth = 1; depth < 12; ++depth) {
+    v3 fpos, fnorm;
+    float fflag;
+    // one trace / shade site for the first ray and the bounces (raygen.rgen:72-126 as one loop: the
+    // first ray starts at tmin 0 and records the HitData position / flag / normal, its radiance is
+    // added only on a hit and without the clamp; bounces update the throughput, roulette from depth 4)
+    for (int depth = 0; depth < 12; ++depth) {
+      if (depth > 0) {
         p.depth = depth;
         thr = thr * p.weight;
         float mt = fmaxx(fmaxx(thr.x, thr.y), thr.z);
@@ -207,15 +204,23 @@ __global__ __launch_bounds__(256) void pt_torus_kernel(DevScene sc, CamParams cp
           if (rnd(p.seed) > pr) break;
           thr = thr / pr;
         }
-        Ray r2 = make_ray(p.next_o, p.next_d, 0.001f, 10000.0f);
-        ext_rays++;
-        Hit h2 = trace_closest<STATS, TEX>(sc, r2, p.seed, c.stack, tc);
-        if (STATS && h2.gid != 0xffffffffu) tc.hits++;
-        ShadowQuery q2;
-        q2.flags = 0;
-        if (h2.gid == 0xffffffffu) miss<true>(cp, p);
-        else closest_hit<true, TEX>(c, p, r2, h2, q2);
-        resolve_shadow<STATS, TEX>(c, p.color, p.seed, q2, tc);
+      }
+      Ray ray = make_ray(p.next_o, p.next_d, depth == 0 ? 0.0f : 0.001f, 10000.0f);
+      ext_rays++;
+      Hit h = trace_closest<STATS, TEX>(sc, ray, p.seed, c.stack, tc);
+      if (STATS && h.gid != 0xffffffffu) tc.hits++;
+      ShadowQuery q;
+      q.flags = 0;
+      if (h.gid == 0xffffffffu) miss<true>(cp, p);
+      else closest_hit<true, TEX>(c, p, ray, h, q);
+      resolve_shadow<STATS, TEX>(c, p.color, p.seed, q, tc);
+      if (depth == 0) {
+        fpos = p.hit_pos;
+        fflag = p.hit_flag;
+        fnorm = p.normal;
+        if (!(p.hit_flag > 0.5f)) break;
+        acc = acc + p.color * thr;
+      } else {
         acc = acc + p.color * thr;
         acc = vmin(acc, 5.0f);
         if (p.hit_flag < 1.5f) break;
