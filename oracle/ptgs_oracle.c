@@ -1661,7 +1661,25 @@ int oracle_splat_gaussians(const float* means, const float* scales, const float*
             }
     }
     free(first);
-    qsort(pairs, (size_t)K, sizeof(OPair), cmp_pair);
+    {   /* the total order of cmp_pair, tile by tile: bucket the pairs by tile (the key's high word),
+         * then sort every tile's bucket with the same comparator in parallel (same result as one
+         * qsort over all K pairs) */
+        const uint32_t nt = (uint32_t)(gx * gy);
+        uint64_t* start = (uint64_t*)calloc((size_t)nt + 1, sizeof(uint64_t));
+        for (uint64_t j = 0; j < K; ++j) start[(uint32_t)(pairs[j].key >> 32) + 1]++;
+        for (uint32_t t = 0; t < nt; ++t) start[t + 1] += start[t];
+        uint64_t* cur = (uint64_t*)malloc(sizeof(uint64_t) * ((size_t)nt + 1));
+        memcpy(cur, start, sizeof(uint64_t) * ((size_t)nt + 1));
+        OPair* bucketed = (OPair*)malloc(sizeof(OPair) * (K ? K : 1));
+        for (uint64_t j = 0; j < K; ++j) bucketed[cur[(uint32_t)(pairs[j].key >> 32)]++] = pairs[j];
+        free(cur);
+        free(pairs);
+        pairs = bucketed;
+#pragma omp parallel for schedule(dynamic, 16)
+        for (int64_t t = 0; t < (int64_t)nt; ++t)
+            if (start[t + 1] - start[t] > 1) qsort(pairs + start[t], (size_t)(start[t + 1] - start[t]), sizeof(OPair), cmp_pair);
+        free(start);
+    }
     uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (K ? K : 1));
     uint32_t* vals = (uint32_t*)malloc(sizeof(uint32_t) * (K ? K : 1));
     for (uint64_t j = 0; j < K; ++j) { keys[j] = pairs[j].key; vals[j] = pairs[j].val; }
