@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-wavefront", action="store_true")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 Cornell-box leg")
     ap.add_argument("--no-torus", action="store_true", help="skip the torus data-collection leg (SURVEY 8f #1)")
+    ap.add_argument("--no-capture", action="store_true", help="skip the dataset capture / export leg (SURVEY 8f #4)")
     ap.add_argument("--no-gs-1m", action="store_true", help="skip the 1M-Gaussian splat and the point-cloud init legs")
     ap.add_argument("--no-gs-10m", action="store_true", help="skip the 10M-Gaussian 3840x2160 splat leg (C5's splat)")
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
@@ -559,6 +560,41 @@ def main():
                         "mrays_per_s": round((tst.extension_rays + tst.shadow_rays) / tdt / 1e6, 1),
                         "msamples_per_s": round(tn * tframes / tdt / 1e6, 1)}
         del tsamp, thits
+
+    # ------------------------------------------------------------------ capture / export
+    # Engine::captureSceneData: views on the toroidal pose sequence, each accumulated on the GPU, sRGB8,
+    # every-2nd-pixel downscale, JPEG q90, transforms_{train,test}.json, then the torus point cloud
+    # (1M RaySamples) -> points3d.ply; 8 of the reference's 336 positions, 128 of its 512 steps
+    if not args.no_pt and not args.no_capture and world == 1:
+        import shutil
+        import tempfile
+        from pathtracer_gaussiansplatting_amd import HITDATA_DTYPE, capture, cornell_box_scene, torus_push
+        csc = cornell_box_scene()
+        csc.blue_noise = Y.blue_noise(1024)
+        r.upload_scene(csc)
+        cubo_c = make_ubo(Camera(aspect=W / H).toroidal(218.6429, 21.5660, 3.5, 3.0), csc, 0, height=H)
+        cn = 1 << 20
+        csamp = torch.from_numpy(np.ascontiguousarray(Y.torus_samples(cn)).view(np.float32)).cuda()
+        cviews, csteps = 8, 128
+        cdir = tempfile.mkdtemp(prefix="ptgs_capture_")
+        try:
+            r.stats_reset(stream)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            capture.capture_dataset(r, cubo_c, cdir, W, H, samples=csamp, num_samples=cn,
+                                    torus_push=torus_push(major_radius=3.5, minor_radius=1.0, height=3.0),
+                                    total_positions=cviews, accumulation_steps=csteps, stream=stream)
+            torch.cuda.synchronize()
+            cdt = time.perf_counter() - t0
+            cst = r.stats()
+            out["capture"] = {"workload": f"dataset capture: C1 Cornell box, {cviews} views at {W}x{H} x {csteps} "
+                                          f"accumulation steps (JPEG q90 at half size, transforms json) + "
+                                          f"{cn}-sample torus point cloud x {csteps} steps -> PLY",
+                              "s_total": round(cdt, 3), "views_per_s": round(cviews / cdt, 2),
+                              "mrays_per_s": round((cst.extension_rays + cst.shadow_rays) / cdt / 1e6, 1)}
+        finally:
+            shutil.rmtree(cdir, ignore_errors=True)
+        del csamp
 
     # ------------------------------------------------------------------ C5: the 8-GPU config
     # 1M-tri atrium + 10M C2-distributed Gaussians in its camera frame, 3840x2160, 256 spp in total.
