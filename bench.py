@@ -407,6 +407,24 @@ def main():
                                           "note": "same frames, alternating between two contexts / streams"}
             r2.close()
             del img2
+            # four views of the C2 Gaussians per call (ptgs_splat_gaussians_views: forked streams, one
+            # workspace per view), the capture-loop use: aggregate Gaussians x views per second
+            vubos = [make_ubo(Camera(aspect=W / H).look_at([0.25 * k, 0.0, 0.0], [0.25 * k, 0.0, -1.0]),
+                              cornell_box_scene(), 0) for k in range(4)]
+            vouts = [torch.zeros_like(img) for _ in vubos]
+            for _ in range(3):
+                r.splat_gaussians_views(dg, vubos, W, H, vouts, stream=stream)
+            torch.cuda.synchronize()
+            vsteps = max(gsteps // 4, 25)
+            t0 = time.perf_counter()
+            for _ in range(vsteps):
+                r.splat_gaussians_views(dg, vubos, W, H, vouts, stream=stream)
+            torch.cuda.synchronize()
+            vdt = (time.perf_counter() - t0) / vsteps
+            out["gs"]["views4"] = {"value": round(N * len(vubos) / vdt / 1e9, 4), "unit": "Gsplats/s",
+                                   "ms_per_call": round(vdt * 1e3, 4),
+                                   "note": "4 camera views of the C2 Gaussians per ptgs_splat_gaussians_views call"}
+            del vouts
         del dg
         # the same forward at the C4 hybrid's Gaussian count (1M), splat only
         if world == 1 and not args.no_gs_1m:

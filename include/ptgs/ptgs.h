@@ -357,6 +357,17 @@ int ptgs_splat_gaussians(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo*
                          uint32_t tile_row_begin, uint32_t tile_row_end, float* out_rgba32f,
                          ptgs_splat_stats* stats, void* hip_stream);
 
+/* Several views of the same Gaussians in one call (the capture loop renders views of one scene):
+ * view v = ptgs_splat_gaussians(ctx, g, &ubos[v], width, height, bg, 0, ~0u, outs[v], NULL, ...),
+ * identical output. Stream-ordered: the views start after the work already on hip_stream, run
+ * concurrently on context-owned streams and workspaces (view 0 on hip_stream), and later work on
+ * hip_stream waits for all of them. n_views in [1, PTGS_MAX_VIEWS]. Not a replacement of
+ * ptgs_splat_gaussians in ptgs_splat_get_buffers: the buffers are view 0's. */
+#define PTGS_MAX_VIEWS 8
+int ptgs_splat_gaussians_views(ptgs_ctx* ctx, const ptgs_gaussians* g, uint32_t n_views, const ptgs_ubo* ubos,
+                               uint32_t width, uint32_t height, const float bg[3], float* const* outs,
+                               void* hip_stream);
+
 /* Hybrid composite (C4): the same splat, front to back over an image: a pixel stops at the first
  * Gaussian whose view depth is >= depth[pixel] (the mesh occludes it and everything behind), and
  * out = C + T * under (all four channels, C.a = 1 - T). depth: device float[W*H] (e.g. from

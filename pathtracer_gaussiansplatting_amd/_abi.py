@@ -183,6 +183,8 @@ SYMBOLS = {
     "ptgs_splat_points": (_I, [_P, C.POINTER(Ubo), C.POINTER(RayPush), _P, _P, _U, _U, _U, _P, _P, _P]),
     "ptgs_splat_gaussians": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _FP, _U, _U, _P,
                                   C.POINTER(SplatStats), _P]),
+    "ptgs_splat_gaussians_views": (_I, [_P, C.POINTER(Gaussians), _U, C.POINTER(Ubo), _U, _U, _FP,
+                                        C.POINTER(C.c_void_p), _P]),
     "ptgs_splat_gaussians_over": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _P, _P, _U, _U, _P,
                                        C.POINTER(SplatStats), _P]),
     "ptgs_splat_get_buffers": (_I, [_P, C.POINTER(SplatBuffers)]),

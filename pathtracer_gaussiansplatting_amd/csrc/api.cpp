@@ -45,6 +45,11 @@ struct ptgs_ctx {
   ptgs_scene_info info{};
   unsigned long long* counters = nullptr;  // 8 x u64
   SplatWorkspace* splat = nullptr;
+  // ptgs_splat_gaussians_views: views 1.. run on their own workspaces and non-blocking streams,
+  // forked from / joined back into the caller's stream with events (view 0 uses `splat` on it)
+  SplatWorkspace* view_ws[PTGS_MAX_VIEWS] = {};
+  hipStream_t view_stream[PTGS_MAX_VIEWS] = {};
+  hipEvent_t view_fork = nullptr, view_join[PTGS_MAX_VIEWS] = {};
   ptgs::WfWorkspace wf;  // wavefront path tracer buffers (PTGS_FLAG_PT_WAVEFRONT)
   void* comm = nullptr;  // RCCL communicator (ptgs_comm_create)
   int comm_ranks = 0, comm_rank = 0;
@@ -153,6 +158,12 @@ void ptgs_destroy(ptgs_ctx* c) {
   if (c->counters) (void)hipFree(c->counters);
   ptgs::wf_workspace_free(c->wf);
   splat_workspace_destroy(c->splat);
+  for (int v = 0; v < PTGS_MAX_VIEWS; ++v) {
+    if (c->view_ws[v]) splat_workspace_destroy(c->view_ws[v]);
+    if (c->view_stream[v]) (void)hipStreamDestroy(c->view_stream[v]);
+    if (c->view_join[v]) (void)hipEventDestroy(c->view_join[v]);
+  }
+  if (c->view_fork) (void)hipEventDestroy(c->view_fork);
   if (c->comm) (void)comm_destroy(c->comm);
   delete c;
 }
@@ -623,6 +634,37 @@ int ptgs_splat_gaussians_over(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_u
   if (!c || !g || !ubo || !out || !depth || !under_rgba32f) return fail(c, PTGS_EINVAL, "null argument");
   const float zero[3] = {0.0f, 0.0f, 0.0f};
   return splat_common(c, g, ubo, w, h, zero, depth, under_rgba32f, tile_row_begin, tile_row_end, out, stats, stream);
+}
+
+int ptgs_splat_gaussians_views(ptgs_ctx* c, const ptgs_gaussians* g, uint32_t n_views, const ptgs_ubo* ubos,
+                               uint32_t w, uint32_t h, const float bg[3], float* const* outs, void* stream) {
+  if (!c || !g || !ubos || !outs || !bg) return fail(c, PTGS_EINVAL, "null argument");
+  if (n_views == 0 || n_views > PTGS_MAX_VIEWS) return fail(c, PTGS_EINVAL, "n_views %u not in [1, %d]", n_views, PTGS_MAX_VIEWS);
+  for (uint32_t v = 0; v < n_views; ++v)
+    if (!outs[v]) return fail(c, PTGS_EINVAL, "null output of view %u", v);
+  if (n_views == 1) return splat_common(c, g, &ubos[0], w, h, bg, nullptr, nullptr, 0, ~0u, outs[0], nullptr, stream);
+  HIPCHK(c, hipSetDevice(c->device));
+  const hipStream_t s = (hipStream_t)stream;
+  if (!c->view_fork) HIPCHK(c, hipEventCreateWithFlags(&c->view_fork, hipEventDisableTiming));
+  for (uint32_t v = 1; v < n_views; ++v) {
+    if (!c->view_ws[v]) c->view_ws[v] = splat_workspace_create();
+    if (!c->view_stream[v]) HIPCHK(c, hipStreamCreateWithFlags(&c->view_stream[v], hipStreamNonBlocking));
+    if (!c->view_join[v]) HIPCHK(c, hipEventCreateWithFlags(&c->view_join[v], hipEventDisableTiming));
+  }
+  HIPCHK(c, hipEventRecord(c->view_fork, s));  // the views start after the caller's earlier work
+  for (uint32_t v = 1; v < n_views; ++v) {
+    HIPCHK(c, hipStreamWaitEvent(c->view_stream[v], c->view_fork, 0));
+    SplatWorkspace* keep = c->splat;
+    c->splat = c->view_ws[v];
+    const int rc = splat_common(c, g, &ubos[v], w, h, bg, nullptr, nullptr, 0, ~0u, outs[v], nullptr, c->view_stream[v]);
+    c->splat = keep;
+    if (rc != PTGS_OK) return rc;
+    HIPCHK(c, hipEventRecord(c->view_join[v], c->view_stream[v]));
+  }
+  const int rc = splat_common(c, g, &ubos[0], w, h, bg, nullptr, nullptr, 0, ~0u, outs[0], nullptr, stream);
+  if (rc != PTGS_OK) return rc;
+  for (uint32_t v = 1; v < n_views; ++v) HIPCHK(c, hipStreamWaitEvent(s, c->view_join[v], 0));  // join
+  return PTGS_OK;
 }
 
 int ptgs_splat_get_buffers(const ptgs_ctx* c, ptgs_splat_buffers* out) {

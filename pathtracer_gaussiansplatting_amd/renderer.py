@@ -214,6 +214,23 @@ class Renderer:
         self._chk(rc, "ptgs_splat_gaussians")
         return st if want_stats else None
 
+    def splat_gaussians_views(self, g: dict, ubos, width: int, height: int, outs, bg=(0.0, 0.0, 0.0), stream=None):
+        """ptgs_splat_gaussians_views: len(ubos) views of the same Gaussians in one stream-ordered call
+        (outs: one RGBA32F[H, W, 4] device tensor per view)."""
+        n = len(ubos)
+        if len(outs) != n:
+            raise ValueError("one output per view")
+        gs = Gaussians()
+        gs.means, gs.scales, gs.rotations = _ptr(g["means"]), _ptr(g["scales"]), _ptr(g["rotations"])
+        gs.opacities, gs.colors = _ptr(g["opacities"]), _ptr(g["colors"])
+        gs.count = int(g["means"].shape[0])
+        bgc = np.asarray(bg, np.float32)
+        arr = (Ubo * n)(*ubos)
+        optrs = (C.c_void_p * n)(*[_ptr(o) for o in outs])
+        rc = self.lib.ptgs_splat_gaussians_views(self._h, C.byref(gs), n, arr, width, height, _abi.fptr(bgc), optrs,
+                                                 _stream(stream))
+        self._chk(rc, "ptgs_splat_gaussians_views")
+
     def bvh_buffers(self) -> BvhBuffers:
         """Device pointers of the uploaded 4-wide BVH nodes and leaf-order triangle records."""
         b = BvhBuffers()

@@ -135,6 +135,30 @@ def test_gaussians_tile_size_boundaries(renderer, oracle_lib):
         assert err < 1e-4, (frame, err)
 
 
+def test_gaussians_views_equal_single_view(renderer):
+    """ptgs_splat_gaussians_views: four cameras of one Gaussian set in one call (views on forked
+    streams and their own workspaces) give each view's single-call image bit for bit, and later work
+    on the caller's stream sees every view complete."""
+    W, H = 320, 180
+    g = {k: _dev(v) for k, v in Y.gaussians_c2(20000, seed=9).items()}
+    sc = U.cornell()
+    ubos = [make_ubo(Camera(aspect=W / H).look_at([0.3 * k, 0.1 * k, 0.0], [0.1 * k, 0.0, -1.0]), sc, 0)
+            for k in range(4)]
+    singles = []
+    for u in ubos:
+        o = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        renderer.splat_gaussians(g, u, W, H, o, bg=(0.1, 0.2, 0.3), want_stats=True)
+        singles.append(o)
+    for _ in range(2):  # the second call reuses the views' workspaces
+        outs = [torch.full((H, W, 4), -1.0, dtype=torch.float32, device="cuda") for _ in ubos]
+        renderer.splat_gaussians_views(g, ubos, W, H, outs, bg=(0.1, 0.2, 0.3))
+        sums = torch.stack([o.sum() for o in outs])  # enqueued on the caller's stream after the join
+        torch.cuda.synchronize()
+        for k in range(len(ubos)):
+            assert torch.equal(outs[k], singles[k]), k
+        assert torch.allclose(sums, torch.stack([o.sum() for o in singles]))
+
+
 def test_gaussians_beyond_24bit_indices(renderer, oracle_lib):
     """2^24 + 3 Gaussians (the register sort packs the gaussian index in 24 bits): every tile goes
     through the LDS rank-count / radix sorts instead; 3000 visible, the rest behind the camera."""
