@@ -140,6 +140,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def assert_complete(rr, where: str) -> int:
+        # every timed splat frame must have been rendered: the stream-ordered splat skips a frame whose
+        # pair count exceeds its buffer (ptgs_splat_status_read counts them); a skipped frame would make
+        # the timed loop cheaper than real work, so the bench refuses to report it
+        skipped = int(rr.splat_status(stream).frames)
+        if skipped:
+            raise SystemExit(f"bench: {skipped} splat frame(s) skipped in {where} (pair buffer too small)")
+        return skipped
+
     def sum_over_ranks(x: float) -> float:
         if world == 1:
             return x
@@ -335,6 +344,7 @@ def main():
 
         for _ in range(max(args.warmup, 1)):
             gs_step()
+        r.splat_status(stream)  # (clears: warm-up frames may have grown the buffers)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -343,6 +353,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         gdt = max_over_ranks(time.perf_counter() - t0)
+        assert_complete(r, "C2 timed loop")
         # per-stage split (separate, untimed pass: the stage events themselves cost ~40 us per frame)
         r.set_flags(FLAG_TIME_STAGES)
         stages = np.zeros(6)
@@ -359,6 +370,7 @@ def main():
         out["gs"] = {
             "value": round(N / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
             "workload": f"C2 3DGS forward: {N} synthetic Gaussians, {W}x{H}", "pairs_K": int(K),
+            "skipped_frames": 0,  # checked after every timed splat loop (ptgs_splat_status_read)
             "scaling": "strong", "parallelism": "single GPU" if world == 1 else
             f"tile-row shard x{world} (rows balanced by pair counts: {gs_rows}) + row gather to rank 0"
             + (" (ptgs_gather_rows, RCCL)" if native_comm else " (gloo rehearsal, host copies)"),
@@ -393,6 +405,8 @@ def main():
                 rk, sk, ik = pipes[k % 2]
                 rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
             torch.cuda.synchronize()
+            r.splat_status(stream)
+            r2.splat_status(s2)
             barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -402,6 +416,8 @@ def main():
             torch.cuda.synchronize()
             barrier()
             g2dt = max_over_ranks(time.perf_counter() - t0)
+            assert_complete(r, "two_in_flight")
+            assert_complete(r2, "two_in_flight (second context)")
             out["gs"]["two_in_flight"] = {"value": round(N * world / (g2dt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
                                           "ms_per_step": round(g2dt / gsteps * 1e3, 4),
                                           "note": "same frames, alternating between two contexts / streams"}
@@ -415,12 +431,14 @@ def main():
             for _ in range(3):
                 r.splat_gaussians_views(dg, vubos, W, H, vouts, stream=stream)
             torch.cuda.synchronize()
+            r.splat_status(stream)
             vsteps = max(gsteps // 4, 25)
             t0 = time.perf_counter()
             for _ in range(vsteps):
                 r.splat_gaussians_views(dg, vubos, W, H, vouts, stream=stream)
             torch.cuda.synchronize()
             vdt = (time.perf_counter() - t0) / vsteps
+            assert_complete(r, "views4")
             out["gs"]["views4"] = {"value": round(N * len(vubos) / vdt / 1e9, 4), "unit": "Gsplats/s",
                                    "ms_per_call": round(vdt * 1e3, 4),
                                    "note": "4 camera views of the C2 Gaussians per ptgs_splat_gaussians_views call"}
@@ -433,11 +451,13 @@ def main():
             for _ in range(2):
                 r.splat_gaussians(g1, gubo, W, H, img, stream=stream)
             torch.cuda.synchronize()
+            r.splat_status(stream)
             t0 = time.perf_counter()
             for _ in range(gsteps):
                 r.splat_gaussians(g1, gubo, W, H, img, stream=stream)
             torch.cuda.synchronize()
             d1 = (time.perf_counter() - t0) / gsteps
+            assert_complete(r, "gs_1m")
             st1 = r.splat_gaussians(g1, gubo, W, H, img, want_stats=True, stream=stream)
             out["gs_1m"] = {"workload": f"3DGS forward only: {args.hybrid_gaussians} C2-distributed Gaussians, {W}x{H}",
                             "value": round(args.hybrid_gaussians / d1 / 1e9, 4), "unit": "Gsplats/s",
@@ -470,12 +490,14 @@ def main():
             for _ in range(3):
                 r.splat_gaussians(g5, g5ubo, W5, H5, img5, stream=stream)
             torch.cuda.synchronize()
+            r.splat_status(stream)
             n5 = 5
             t0 = time.perf_counter()
             for _ in range(n5):
                 r.splat_gaussians(g5, g5ubo, W5, H5, img5, stream=stream)
             torch.cuda.synchronize()
             d5 = (time.perf_counter() - t0) / n5
+            assert_complete(r, "gs_10m_4k")
             st5 = r.splat_gaussians(g5, g5ubo, W5, H5, img5, want_stats=True, stream=stream)
             out["gs_10m_4k"] = {"workload": f"C5 splat on one GPU: {N5} C2-distributed Gaussians, {W5}x{H5}",
                                 "value": round(N5 / d5 / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(d5 * 1e3, 3),
@@ -495,17 +517,18 @@ def main():
         hdepth = torch.zeros((H, W), dtype=torch.float32, device="cuda")
         hframe = 0
 
-        def hybrid_step():
+        def hybrid_step(want_stats=False):
             nonlocal hframe
             hubo = make_ubo(pose, scene, hframe, ambient=(0.3, 0.4, 0.5, 1.0), height=H)
             r.trace_camera(hubo, W, H, haccum, spp=args.hybrid_spp, stream=stream)
             r.trace_depth(hubo, W, H, hdepth, stream=stream)
-            r.splat_gaussians(hdg, hubo, W, H, haccum, over=(hdepth, haccum), stream=stream)
+            r.splat_gaussians(hdg, hubo, W, H, haccum, over=(hdepth, haccum), want_stats=want_stats, stream=stream)
             hframe += args.hybrid_spp
 
-        for _ in range(max(args.warmup, 1)):
-            hybrid_step()
+        for k in range(max(args.warmup, 1)):
+            hybrid_step(want_stats=k == 0)  # the first sizes the pair buffer
         torch.cuda.synchronize()
+        r.splat_status(stream)
         r.stats_reset(stream)
         hsteps = max(args.steps, 3)
         t0 = time.perf_counter()
@@ -513,6 +536,7 @@ def main():
             hybrid_step()
         torch.cuda.synchronize()
         hdt = (time.perf_counter() - t0) / hsteps
+        assert_complete(r, "hybrid")
         hst = r.stats()
         out["hybrid"] = {
             "workload": f"C4 hybrid: {args.hybrid_gaussians} C2-distributed Gaussians + the C3 mesh, {W}x{H}, "
@@ -637,7 +661,7 @@ def main():
         comp5 = torch.zeros((H5, W5, 4), dtype=torch.float32, device="cuda")
         rows5 = D.tile_row_shard(rank, world, H5)
 
-        def c5_frame():
+        def c5_frame(want_stats=False):
             u5 = make_ubo(pose5, sc5, rank, ambient=(0.3, 0.4, 0.5, 1.0), height=H5)
             acc5.zero_()
             r.trace_camera(u5, W5, H5, acc5, spp=SPP5 // world, frame_stride=world, mode=_SUM, stream=stream)
@@ -649,11 +673,13 @@ def main():
             r.trace_depth(u5, W5, H5, dep5, stream=stream)
             comp5.zero_()
             if rows5[1] > rows5[0]:
-                r.splat_gaussians(dg5, u5, W5, H5, comp5, tile_rows=rows5, over=(dep5, mean5), stream=stream)
+                r.splat_gaussians(dg5, u5, W5, H5, comp5, tile_rows=rows5, over=(dep5, mean5), want_stats=want_stats,
+                                  stream=stream)
             reduce_to_root(comp5)
 
-        c5_frame()  # warm-up (sort sizes follow the previous frame's tiles)
+        c5_frame(want_stats=True)  # warm-up: sizes the pair buffer (sort sizes follow the previous frame's tiles)
         torch.cuda.synchronize()
+        r.splat_status(stream)
         r.stats_reset(stream)
         barrier()
         torch.cuda.synchronize()
@@ -662,6 +688,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         d5 = max_over_ranks(time.perf_counter() - t0)
+        assert_complete(r, "c5")
         s5 = r.stats()
         rays5 = sum_over_ranks(float(s5.extension_rays + s5.shadow_rays))
         out["c5"] = {"workload": f"C5: {G5} Gaussians + {int(info5.num_triangles)}-tri mesh, {W5}x{H5}, {SPP5} spp "

@@ -347,11 +347,13 @@ typedef struct ptgs_splat_stats {
  * pixels outside are left untouched.
  * Stream-ordered when stats == NULL: no host synchronisation, so a frame can be captured into and
  * replayed from a hipGraph. The (Gaussian, tile) pair buffer of the context's workspace starts at
- * 8 pairs per Gaussian and grows from the pair counts of earlier frames; a frame whose pair count
- * exceeds it renders incompletely, and the next call grows the buffer (growth frees buffers, which
- * waits for the device and invalidates graphs captured before it: capture after a frame with stats).
+ * 8 pairs per Gaussian (or ptgs_splat_reserve's size) and grows from the pair counts of earlier
+ * frames. A frame whose pair count exceeds it is SKIPPED on the device (out is left untouched) and
+ * counted: ptgs_splat_status reports every skipped frame, and the next call grows the buffer
+ * (growth frees buffers, which waits for the device and invalidates graphs captured before it:
+ * reserve, or capture after a frame with stats).
  * stats != NULL: the call waits for the frame's pair count, re-runs it after growing the buffer when
- * it did not fit (the frame is always complete) and fills stats. */
+ * it did not fit (the frame is always complete and never counted as skipped) and fills stats. */
 int ptgs_splat_gaussians(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo* ubo,
                          uint32_t width, uint32_t height, const float bg[3],
                          uint32_t tile_row_begin, uint32_t tile_row_end, float* out_rgba32f,
@@ -367,6 +369,26 @@ int ptgs_splat_gaussians(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo*
 int ptgs_splat_gaussians_views(ptgs_ctx* ctx, const ptgs_gaussians* g, uint32_t n_views, const ptgs_ubo* ubos,
                                uint32_t width, uint32_t height, const float bg[3], float* const* outs,
                                void* hip_stream);
+
+/* Skipped-frame report of the stream-ordered splat (no stats): waits for hip_stream and the
+ * context's view streams, then returns and clears the number of frames skipped since the last query
+ * because their pair count exceeded the pair buffer. views[v]: frames of view slot v (slot 0 counts
+ * ptgs_splat_gaussians / _over and view 0 of ptgs_splat_gaussians_views); frames = their sum.
+ * pair_capacity: the smallest pair capacity over the slots in use; last_pairs: the largest pair count
+ * any slot's latest frame produced. A frame reported here left its output untouched: render it
+ * again (the buffers have grown by then), or call with stats. */
+typedef struct ptgs_splat_status {
+    uint64_t frames;
+    uint32_t views[PTGS_MAX_VIEWS];
+    uint32_t pair_capacity;
+    uint32_t last_pairs;
+} ptgs_splat_status;
+int ptgs_splat_status_read(ptgs_ctx* ctx, ptgs_splat_status* out, void* hip_stream);
+
+/* Grow the pair buffers of every view slot to at least `pairs` (Gaussian, tile) pairs so that
+ * stream-ordered frames up to that count are never skipped (e.g. before capturing a hipGraph, or
+ * from a previous frame's stats.num_rendered plus headroom). Synchronises the device when it grows. */
+int ptgs_splat_reserve(ptgs_ctx* ctx, uint32_t pairs);
 
 /* Hybrid composite (C4): the same splat, front to back over an image: a pixel stops at the first
  * Gaussian whose view depth is >= depth[pixel] (the mesh occludes it and everything behind), and

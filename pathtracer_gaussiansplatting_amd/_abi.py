@@ -144,6 +144,12 @@ class SplatStats(C.Structure):
                 ("num_visible", C.c_uint32)]
 
 
+class SplatStatus(C.Structure):
+    """ptgs_splat_status: frames the stream-ordered splat skipped (pair buffer too small)."""
+    _fields_ = [("frames", C.c_uint64), ("views", C.c_uint32 * 8), ("pair_capacity", C.c_uint32),
+                ("last_pairs", C.c_uint32)]
+
+
 class SplatBuffers(C.Structure):
     _fields_ = [("radii", C.c_void_p), ("tiles_touched", C.c_void_p), ("sorted_keys", C.c_void_p),
                 ("sorted_values", C.c_void_p), ("tile_ranges", C.c_void_p), ("means2d", C.c_void_p),
@@ -188,6 +194,8 @@ SYMBOLS = {
     "ptgs_splat_gaussians_over": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _P, _P, _U, _U, _P,
                                        C.POINTER(SplatStats), _P]),
     "ptgs_splat_get_buffers": (_I, [_P, C.POINTER(SplatBuffers)]),
+    "ptgs_splat_status_read": (_I, [_P, C.POINTER(SplatStatus), _P]),
+    "ptgs_splat_reserve": (_I, [_P, _U]),
     "ptgs_knn3_mean_dist2": (_I, [_P, _P, _U, _P, _P]),
     "ptgs_gaussians_from_points": (_I, [_P, _P, _P, _U, _P, _P, _P, _P, _P, _P]),
     "ptgs_comm_unique_id": (_I, [_P]),

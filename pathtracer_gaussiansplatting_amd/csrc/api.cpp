@@ -14,6 +14,7 @@
 #endif
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -646,24 +647,72 @@ int ptgs_splat_gaussians_views(ptgs_ctx* c, const ptgs_gaussians* g, uint32_t n_
   HIPCHK(c, hipSetDevice(c->device));
   const hipStream_t s = (hipStream_t)stream;
   if (!c->view_fork) HIPCHK(c, hipEventCreateWithFlags(&c->view_fork, hipEventDisableTiming));
+  // every view's pair buffer starts from the largest pair count any slot has seen (views of one
+  // Gaussian set have similar counts): a fresh view workspace would otherwise start at 8 pairs per
+  // Gaussian and skip its first over-capacity frame (reported by ptgs_splat_status_read)
+  uint32_t hint = splat_pair_hint(c->splat);
   for (uint32_t v = 1; v < n_views; ++v) {
     if (!c->view_ws[v]) c->view_ws[v] = splat_workspace_create();
     if (!c->view_stream[v]) HIPCHK(c, hipStreamCreateWithFlags(&c->view_stream[v], hipStreamNonBlocking));
     if (!c->view_join[v]) HIPCHK(c, hipEventCreateWithFlags(&c->view_join[v], hipEventDisableTiming));
+    hint = std::max(hint, splat_pair_hint(c->view_ws[v]));
+  }
+  if (hint) {
+    const uint32_t want = hint + hint / 8u;  // headroom for the views' differences
+    for (uint32_t v = 1; v < n_views; ++v) HIPCHK(c, splat_reserve(c->view_ws[v], want));
   }
   HIPCHK(c, hipEventRecord(c->view_fork, s));  // the views start after the caller's earlier work
+  // on any failure after a view was forked, the views already launched are joined back into the
+  // caller's stream before returning (later work there must not race them)
+  uint32_t launched = 1;
+  auto join = [&]() {
+    for (uint32_t v = 1; v < launched; ++v) (void)hipStreamWaitEvent(s, c->view_join[v], 0);
+  };
   for (uint32_t v = 1; v < n_views; ++v) {
-    HIPCHK(c, hipStreamWaitEvent(c->view_stream[v], c->view_fork, 0));
+    hipError_t e = hipStreamWaitEvent(c->view_stream[v], c->view_fork, 0);
+    if (e != hipSuccess) { join(); return fail(c, PTGS_EHIP, "hipStreamWaitEvent: %s", hipGetErrorString(e)); }
     SplatWorkspace* keep = c->splat;
     c->splat = c->view_ws[v];
     const int rc = splat_common(c, g, &ubos[v], w, h, bg, nullptr, nullptr, 0, ~0u, outs[v], nullptr, c->view_stream[v]);
     c->splat = keep;
-    if (rc != PTGS_OK) return rc;
-    HIPCHK(c, hipEventRecord(c->view_join[v], c->view_stream[v]));
+    // (record the join even after a failed view: kernels it did enqueue must be waited for)
+    e = hipEventRecord(c->view_join[v], c->view_stream[v]);
+    if (e == hipSuccess) launched = v + 1;
+    if (rc != PTGS_OK) { join(); return rc; }
+    if (e != hipSuccess) { join(); return fail(c, PTGS_EHIP, "hipEventRecord: %s", hipGetErrorString(e)); }
   }
   const int rc = splat_common(c, g, &ubos[0], w, h, bg, nullptr, nullptr, 0, ~0u, outs[0], nullptr, stream);
-  if (rc != PTGS_OK) return rc;
-  for (uint32_t v = 1; v < n_views; ++v) HIPCHK(c, hipStreamWaitEvent(s, c->view_join[v], 0));  // join
+  join();
+  return rc;
+}
+
+int ptgs_splat_status_read(ptgs_ctx* c, ptgs_splat_status* out, void* stream) {
+  if (!c || !out) return PTGS_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+  for (int v = 1; v < PTGS_MAX_VIEWS; ++v)
+    if (c->view_stream[v]) HIPCHK(c, hipStreamSynchronize(c->view_stream[v]));
+  *out = ptgs_splat_status{};
+  out->pair_capacity = 0xFFFFFFFFu;
+  for (int v = 0; v < PTGS_MAX_VIEWS; ++v) {
+    SplatWorkspace* ws = v == 0 ? c->splat : c->view_ws[v];
+    if (!ws) continue;
+    uint32_t skipped = 0, cap = 0, last = 0;
+    splat_status(ws, true, &skipped, &cap, &last);
+    out->views[v] = skipped;
+    out->frames += skipped;
+    out->pair_capacity = std::min(out->pair_capacity, cap);
+    out->last_pairs = std::max(out->last_pairs, last);
+  }
+  return PTGS_OK;
+}
+
+int ptgs_splat_reserve(ptgs_ctx* c, uint32_t pairs) {
+  if (!c) return PTGS_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, splat_reserve(c->splat, pairs));
+  for (int v = 1; v < PTGS_MAX_VIEWS; ++v)
+    if (c->view_ws[v]) HIPCHK(c, splat_reserve(c->view_ws[v], pairs));
   return PTGS_OK;
 }
 

@@ -600,7 +600,7 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   a.tiles_x = (W + 7u) / 8u;
   a.stride = stride;
   const uint32_t tiles = a.tiles_x * ((row1 - row0 + 7u) / 8u);
-  // samples per batch: up to batch_max, within ~2^25 slots (161 B each: 5.4 GB at the cap)
+  // samples per batch: up to batch_max, within ~2^25 slots (145 B each: 4.9 GB at the cap)
   const uint32_t bcap = std::max(1u, (uint32_t)((1u << 25) / ((size_t)tiles * 64u)));
   const uint32_t bmax = std::min({batch_max, spp, bcap});
   const size_t Pmax = (size_t)tiles * 64u * bmax;
@@ -608,8 +608,8 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   const uint32_t grid_pmax = (uint32_t)((Pmax + 255u) / 256u);
   a.part_stride = grid_pmax;  // the largest grid of any stage (runs are >= 64 slots per wave)
   hipError_t e;
-  // 10 float4 + 1 flag byte per slot
-  if ((e = wf_ensure(w.slots, w.slots_bytes, Pmax * (10 * 16 + 1), false, s))) return e;
+  // 9 float4 streams (ray o / d, hit, shadow o / d / acc, path throughput / weight / acc) + 1 flag byte per slot
+  if ((e = wf_ensure(w.slots, w.slots_bytes, Pmax * (9 * 16 + 1), false, s))) return e;
   // the per-depth "work pending" words (2 per depth), then the partial counts [WF_NCNT][part_stride]
   if ((e = wf_ensure(w.part, w.part_bytes, ((size_t)WF_NCNT * a.part_stride + 64) * 4, true, s))) return e;
   {  // traversal-stack overflow: the entries beyond the LDS part, per work-item of the largest grid
@@ -623,7 +623,7 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   a.ray_o = f; a.ray_d = f + P; a.hits = f + 2 * P;
   a.sh_o = f + 3 * P; a.sh_d = f + 4 * P; a.sh_acc = f + 5 * P;
   a.st_thr = f + 6 * P; a.st_w = f + 7 * P; a.st_acc = f + 8 * P;
-  a.flags = (uint8_t*)(f + 10 * P);
+  a.flags = (uint8_t*)(f + 9 * P);
   // the "work pending" words first: at a fixed offset, so a later call with a larger grid (stride)
   // never counts a previous call's flags as partial ray counts
   a.live = (uint32_t*)w.part;

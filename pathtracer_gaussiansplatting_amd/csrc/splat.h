@@ -19,6 +19,13 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
                            ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s);
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
+// grow the pair buffers to at least `pairs` (frees / reallocates: waits for the device)
+hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs);
+// frames skipped on the device (pair count above the buffer) since the last clear; the pair
+// capacity; the latest pair count a frame published (call after the workspace's stream has drained)
+void splat_status(SplatWorkspace* w, bool clear, uint32_t* skipped, uint32_t* capacity, uint32_t* last_pairs);
+// the latest pair count any frame of this workspace published (a hint: no wait)
+uint32_t splat_pair_hint(const SplatWorkspace* w);
 void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out);
 hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long** keys);
 

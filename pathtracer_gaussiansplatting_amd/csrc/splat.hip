@@ -510,6 +510,9 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);      // largest tile (the next sort's LDS size)
     __atomic_store_n(k_host + 2, large_ctr[0], __ATOMIC_RELAXED);  // large tiles (the next sort grid)
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
+    // a frame that does not fit is skipped by this kernel, the sort and the blend: count it for
+    // ptgs_splat_status_read (one writer per workspace: its frames are ordered on one stream)
+    if (carry > cap) __atomic_store_n(k_host + 3, __atomic_load_n(k_host + 3, __ATOMIC_RELAXED) + 1u, __ATOMIC_RELAXED);
     __threadfence_system();  // visible to the host before the kernel ends (the K event has no system fence)
   }
   if (carry > cap) return;
@@ -1369,6 +1372,9 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = hipEventSynchronize(w->k_event))) return e;
     K = w->k_host[0];
     if (K > cap_now()) {  // did not fit: grow and re-run scatter, sort and blend
+      // (the device counted the skipped attempt; this frame will be complete: uncount it. Every
+      // earlier frame of this workspace has finished, so no device write of the word is pending)
+      if (w->k_host[3]) w->k_host[3] -= 1u;
       if ((e = grow(K))) return e;
       if ((e = mark(2))) return e;
       if ((e = enqueue_tail(cap_now()))) return e;
@@ -1390,6 +1396,24 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   w->last_published = publish && stats;
   return hipSuccess;
 }
+
+hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs) {
+  hipError_t e;
+  if ((e = ensure(w->pairs, (size_t)pairs * 8))) return e;
+  if ((e = ensure(w->vals_out, (size_t)pairs * 4))) return e;
+  if (w->keys_out.p && (e = ensure(w->keys_out, (size_t)pairs * 8))) return e;
+  return hipSuccess;
+}
+
+void splat_status(SplatWorkspace* w, bool clear, uint32_t* skipped, uint32_t* capacity, uint32_t* last_pairs) {
+  *skipped = w->k_host ? w->k_host[3] : 0u;
+  if (clear && w->k_host) w->k_host[3] = 0u;
+  const size_t c = std::min(w->pairs.bytes / 8, w->vals_out.bytes / 4);
+  *capacity = (uint32_t)std::min<size_t>(c, 0xFFFFFFFFu);
+  *last_pairs = w->k_host ? w->k_host[0] : 0u;
+}
+
+uint32_t splat_pair_hint(const SplatWorkspace* w) { return w->k_host ? w->k_host[0] : 0u; }
 
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms) {
   for (int k = 0; k < 6; ++k) out_ms[k] = 0.0f;

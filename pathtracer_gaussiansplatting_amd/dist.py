@@ -80,25 +80,50 @@ def all_reduce_sum(tensor, group=None):
     return tensor
 
 
-def gather_rows(image, pixel_ranges, dst: int = 0, renderer=None, group=None):
+def gather_rows(image, pixel_ranges, dst: int = 0, renderer=None, group=None, stream=None):
     """Every rank's pixel rows [r0, r1) of image ((H, W, 4) float32) to the same rows of dst's image.
-    Through the library's communicator when the renderer has one, else torch.distributed send/recv."""
+    Through the library's communicator when the renderer has one (ordered on `stream`), else
+    torch.distributed send/recv, issued after the work already on `stream` (the rows it renders)."""
     import torch.distributed as dist
     if not (dist.is_initialized() and dist.get_world_size(group) > 1):
         return image
+    if len(pixel_ranges) != dist.get_world_size(group):
+        raise ValueError("gather_rows needs one (r0, r1) per rank")
     if renderer is not None and getattr(renderer, "comm_world", 0) > 1:
-        renderer.gather_rows(image, pixel_ranges, root=dst)
+        renderer.gather_rows(image, pixel_ranges, root=dst, stream=stream)
         return image
-    rank = dist.get_rank(group)
-    if rank == dst:
-        for g, (r0, r1) in enumerate(pixel_ranges):
-            if g != dst and r1 > r0:
-                dist.recv(image[r0:r1], src=g, group=group)
-    else:
-        r0, r1 = pixel_ranges[rank]
-        if r1 > r0:
-            dist.send(image[r0:r1].contiguous(), dst=dst, group=group)
+    with _on_stream(image, stream):
+        rank = dist.get_rank(group)
+        if rank == dst:
+            for g, (r0, r1) in enumerate(pixel_ranges):
+                if g != dst and r1 > r0:
+                    dist.recv(image[r0:r1], src=g, group=group)
+        else:
+            r0, r1 = pixel_ranges[rank]
+            if r1 > r0:
+                dist.send(image[r0:r1].contiguous(), dst=dst, group=group)
     return image
+
+
+class _on_stream:
+    """torch.cuda.stream(stream) for device tensors (collectives issued after the stream's work);
+    nothing for host tensors or stream=None."""
+
+    def __init__(self, tensor, stream):
+        self.ctx = None
+        if stream is not None and not isinstance(stream, int) and getattr(tensor, "is_cuda", False):
+            import torch
+            self.ctx = torch.cuda.stream(stream)
+
+    def __enter__(self):
+        if self.ctx is not None:
+            self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            return self.ctx.__exit__(*exc)
+        return False
 
 
 def init_native_comm(renderer, group=None):
@@ -148,4 +173,4 @@ def render_gaussian_frame(renderer, gaussians: dict, ubo, width: int, height: in
     rows = tile_rows[rank]
     if rows[1] > rows[0]:
         renderer.splat_gaussians(gaussians, ubo, width, height, out, bg=bg, tile_rows=rows, stream=stream)
-    return gather_rows(out, [pixel_rows(r, height) for r in tile_rows], dst=0, renderer=renderer)
+    return gather_rows(out, [pixel_rows(r, height) for r in tile_rows], dst=0, renderer=renderer, stream=stream)

@@ -16,7 +16,7 @@ import ctypes as C
 import numpy as np
 
 from . import _abi
-from ._abi import BvhBuffers, Gaussians, RayPush, SceneInfo, SplatBuffers, SplatStats, TraceStats, Ubo
+from ._abi import BvhBuffers, Gaussians, RayPush, SceneInfo, SplatBuffers, SplatStats, SplatStatus, TraceStats, Ubo
 
 
 def _ptr(x) -> int:
@@ -164,7 +164,12 @@ class Renderer:
         """Every rank's pixel rows [r0, r1) of the (H, W, 4) float32 image to root (ptgs_gather_rows);
         row_ranges: one (r0, r1) per rank, identical on every rank."""
         H, W = int(image.shape[0]), int(image.shape[1])
+        world = getattr(self, "comm_world", 0)
+        if len(row_ranges) != world:  # the library reads 2 x nranks entries
+            raise ValueError(f"gather_rows needs one (r0, r1) per rank: {len(row_ranges)} given, world {world}")
         rr = np.asarray(row_ranges, np.uint32).reshape(-1)
+        if rr.size != 2 * world:
+            raise ValueError("gather_rows: every row range is a (r0, r1) pair")
         rc = self.lib.ptgs_gather_rows(self._h, _ptr(image), W, H, rr.ctypes.data, root, _stream(stream))
         self._chk(rc, "ptgs_gather_rows")
 
@@ -230,6 +235,17 @@ class Renderer:
         rc = self.lib.ptgs_splat_gaussians_views(self._h, C.byref(gs), n, arr, width, height, _abi.fptr(bgc), optrs,
                                                  _stream(stream))
         self._chk(rc, "ptgs_splat_gaussians_views")
+
+    def splat_status(self, stream=None) -> SplatStatus:
+        """ptgs_splat_status_read: waits for `stream` and the view streams, returns and clears the
+        count of splat frames skipped because their pair count exceeded the pair buffer."""
+        st = SplatStatus()
+        self._chk(self.lib.ptgs_splat_status_read(self._h, C.byref(st), _stream(stream)), "ptgs_splat_status_read")
+        return st
+
+    def splat_reserve(self, pairs: int):
+        """Grow every view slot's pair buffer to at least `pairs` (no skipped frames up to that count)."""
+        self._chk(self.lib.ptgs_splat_reserve(self._h, int(pairs)), "ptgs_splat_reserve")
 
     def bvh_buffers(self) -> BvhBuffers:
         """Device pointers of the uploaded 4-wide BVH nodes and leaf-order triangle records."""

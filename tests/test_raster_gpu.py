@@ -214,6 +214,83 @@ def test_gaussians_first_frame_overflow_rerun_published(native_lib, oracle_lib):
         r.close()
 
 
+def test_gaussians_skipped_frame_is_reported(native_lib, oracle_lib):
+    """a stream-ordered frame (no stats) whose pair count exceeds the fresh pair
+    buffer (8 per Gaussian) is skipped on the device; ptgs_splat_status_read must report it (and
+    clear), the output must be untouched, and the next call (buffers grown from the published pair
+    count) must render the oracle's frame and report nothing."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H = 256, 144
+    g = Y.gaussians_c2(3000, seed=21)
+    g["scales"] *= 16.0  # K > 10 n: beyond the initial capacity
+    ubo = _gauss_ubo(W, H)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H)
+    assert ref["K"] > 10 * 3000, ref["K"]
+    r = Renderer(0)
+    try:
+        dg = {k: _dev(v) for k, v in g.items()}
+        out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+        r.splat_gaussians(dg, ubo, W, H, out)  # first frame: no stats, does not fit
+        st = r.splat_status()
+        assert st.frames == 1 and st.views[0] == 1, (st.frames, list(st.views))
+        assert st.last_pairs == ref["K"] and st.pair_capacity < ref["K"]
+        assert bool((out == -7.0).all()), "a skipped frame must leave its output untouched"
+        assert r.splat_status().frames == 0  # read-and-clear
+        r.splat_gaussians(dg, ubo, W, H, out)  # grown from the published K: complete
+        st = r.splat_status()
+        assert st.frames == 0 and st.pair_capacity >= ref["K"]
+        assert U.rel_l2(out.cpu().numpy(), ref["image"]) < 1e-4
+        # with stats the over-capacity attempt is re-run inside the call and never reported
+        r2 = Renderer(0)
+        try:
+            out2 = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            s2 = r2.splat_gaussians(dg, ubo, W, H, out2, want_stats=True)
+            assert s2.num_rendered == ref["K"] and r2.splat_status().frames == 0
+            assert torch.equal(out2, out)
+        finally:
+            r2.close()
+    finally:
+        r.close()
+
+
+def test_gaussians_views_skipped_frames_per_view(native_lib, oracle_lib):
+    """fresh view workspaces are sized from the largest pair count any slot has seen, so a
+    views call after one single-view frame renders every view completely; on a fresh context the
+    over-capacity views are reported per view slot, and the next call renders them all."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H = 256, 144
+    g = Y.gaussians_c2(3000, seed=21)
+    g["scales"] *= 16.0
+    dg = {k: _dev(v) for k, v in g.items()}
+    sc = U.cornell()
+    ubos = [make_ubo(Camera(aspect=W / H).look_at([0.05 * k, 0.0, 0.0], [0.05 * k, 0.0, -1.0]), sc, 0)
+            for k in range(3)]
+    refs = [oracle_lib.splat_gaussians(g, u, W, H)["image"] for u in ubos]
+    r = Renderer(0)
+    try:
+        outs = [torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda") for _ in ubos]
+        r.splat_gaussians_views(dg, ubos, W, H, outs)  # fresh context: every view overflows
+        st = r.splat_status()
+        assert st.frames == 3 and list(st.views[:3]) == [1, 1, 1], list(st.views)
+        r.splat_gaussians_views(dg, ubos, W, H, outs)
+        assert r.splat_status().frames == 0
+        for o, ref in zip(outs, refs):
+            assert U.rel_l2(o.cpu().numpy(), ref) < 1e-4
+    finally:
+        r.close()
+    r = Renderer(0)
+    try:
+        one = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        r.splat_gaussians(dg, ubos[0], W, H, one, want_stats=True)  # slot 0 learns K
+        outs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in ubos]
+        r.splat_gaussians_views(dg, ubos, W, H, outs)  # views 1, 2: fresh slots sized from slot 0
+        assert r.splat_status().frames == 0
+        for o, ref in zip(outs, refs):
+            assert U.rel_l2(o.cpu().numpy(), ref) < 1e-4
+    finally:
+        r.close()
+
+
 def test_gaussians_stream_ordered_graph_replay(renderer, oracle_lib):
     """Without stats ptgs_splat_gaussians never waits on the host (ptgs.h): a C2-sized frame (100k
     Gaussians, 1920x1080) is captured into a hipGraph and replayed; the replays reproduce the oracle
