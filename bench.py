@@ -309,7 +309,13 @@ def main():
     # ------------------------------------------------------------------ 3DGS (C2)
     if not args.no_gs:
         g = Y.gaussians_c2(args.gaussians, seed=1)  # one scene: every rank holds all Gaussians
-        dg = {k: torch.from_numpy(v).cuda() for k, v in g.items()}
+        dg0 = {k: torch.from_numpy(v).cuda() for k, v in g.items()}  # the generator's (random) order
+        # scene preparation (untimed, like the BVH build): a copy in 3D Morton order of the means with
+        # the original indices (ptgs_gaussians_sort_spatial); it renders exactly like dg0 (checked below)
+        torch.cuda.synchronize()
+        tprep = time.perf_counter()
+        dg = r.sort_gaussians_spatial(dg0, stream=stream)
+        prep_ms = (time.perf_counter() - tprep) * 1e3
         gpose = Camera(aspect=W / H).look_at([0.0, 0.0, 0.0], [0.0, 0.0, -1.0])
         from pathtracer_gaussiansplatting_amd import cornell_box_scene
         gubo = make_ubo(gpose, cornell_box_scene(), 0)
@@ -354,6 +360,26 @@ def main():
         barrier()
         gdt = max_over_ranks(time.perf_counter() - t0)
         assert_complete(r, "C2 timed loop")
+        # the same frames from the Gaussians in their generated (random) order: the same image bit for
+        # bit, timed alone (secondary figure)
+        img0 = torch.zeros_like(img)
+        r.splat_gaussians(dg0, gubo, W, H, img0, stream=stream)
+        r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
+        torch.cuda.synchronize()
+        same_image = bool(torch.equal(img0, img))
+        if not same_image:
+            raise SystemExit("bench: the spatially ordered Gaussians render a different C2 frame")
+        for _ in range(3):
+            r.splat_gaussians(dg0, gubo, W, H, img0, stream=stream)
+        r.splat_status(stream)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(gsteps):
+            r.splat_gaussians(dg0, gubo, W, H, img0, stream=stream)
+        torch.cuda.synchronize()
+        udt = time.perf_counter() - t0
+        assert_complete(r, "C2 unsorted loop")
+        del img0
         # per-stage split (separate, untimed pass: the stage events themselves cost ~40 us per frame)
         r.set_flags(FLAG_TIME_STAGES)
         stages = np.zeros(6)
@@ -374,9 +400,15 @@ def main():
             "scaling": "strong", "parallelism": "single GPU" if world == 1 else
             f"tile-row shard x{world} (rows balanced by pair counts: {gs_rows}) + row gather to rank 0"
             + (" (ptgs_gather_rows, RCCL)" if native_comm else " (gloo rehearsal, host copies)"),
+            "front_end": "fused single launch" if st.fused else "count + colscan + scatter",
             "stages_ms": {k: round(float(v), 4) for k, v in
-                          zip(["preprocess+count", "colscan", "scatter", "sort_large", "-", "sort_blend"], stages)
-                          if k != "-"},
+                          zip(["front_end" if st.fused else "preprocess+count", "colscan", "scatter", "sort_large",
+                               "-", "sort_blend"], stages) if k != "-" and not (st.fused and k in ("colscan", "scatter"))},
+            "gaussian_order": f"3D Morton order of the means (ptgs_gaussians_sort_spatial, {prep_ms:.2f} ms once, "
+                              "untimed scene preparation; identical image to the generated order, checked)",
+            "unsorted_order": {"value": round(N / (udt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
+                               "ms_per_step": round(udt / gsteps * 1e3, 4),
+                               "note": "the same frames from the Gaussians in their generated (random) order"},
             "roofline": {"bound": "hbm", "kernel": "whole pipeline", "achieved": round(b_gs / (gms * 1e-3) / 1e9, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(b_gs / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "alg_bytes": b_gs},
@@ -446,7 +478,8 @@ def main():
         del dg
         # the same forward at the C4 hybrid's Gaussian count (1M), splat only
         if world == 1 and not args.no_gs_1m:
-            g1 = {k: torch.from_numpy(v).cuda() for k, v in Y.gaussians_c2(args.hybrid_gaussians, seed=3).items()}
+            g1 = r.sort_gaussians_spatial({k: torch.from_numpy(v).cuda()
+                                           for k, v in Y.gaussians_c2(args.hybrid_gaussians, seed=3).items()})
             r.splat_gaussians(g1, gubo, W, H, img, want_stats=True, stream=stream)  # sizes the pair buffer
             for _ in range(2):
                 r.splat_gaussians(g1, gubo, W, H, img, stream=stream)
@@ -479,7 +512,7 @@ def main():
         # global-scratch radix path); the 8-GPU C5 shards these tile rows across ranks (dist.tile_row_shard)
         if world == 1 and not args.no_gs_10m:
             W5, H5, N5 = 3840, 2160, 10_000_000
-            g5 = {k: torch.from_numpy(v).cuda() for k, v in Y.gaussians_c2(N5, seed=5).items()}
+            g5 = r.sort_gaussians_spatial({k: torch.from_numpy(v).cuda() for k, v in Y.gaussians_c2(N5, seed=5).items()})
             img5 = torch.zeros((H5, W5, 4), dtype=torch.float32, device="cuda")
             g5pose = Camera(aspect=W5 / H5).look_at([0.0, 0.0, 0.0], [0.0, 0.0, -1.0])
             g5ubo = make_ubo(g5pose, cornell_box_scene(), 0)
@@ -512,7 +545,7 @@ def main():
     # (hybrid_spp), primary-hit depth, splat over the traced frame (build-defined).
     if not args.no_pt and not args.no_hybrid and world == 1:
         hg = Y.gaussians_in_view(args.hybrid_gaussians, 3, make_ubo(pose, scene, 0, height=H))
-        hdg = {k: torch.from_numpy(v).cuda() for k, v in hg.items()}
+        hdg = r.sort_gaussians_spatial({k: torch.from_numpy(v).cuda() for k, v in hg.items()})
         haccum = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
         hdepth = torch.zeros((H, W), dtype=torch.float32, device="cuda")
         hframe = 0
@@ -654,7 +687,7 @@ def main():
         info5 = r.upload_scene(sc5)
         pose5 = Camera(aspect=W5 / H5).look_at([-15.0, 4.0, 5.0], [10.0, 3.0, -3.0])
         g5 = Y.gaussians_in_view(G5, 5, make_ubo(pose5, sc5, 0, height=H5))
-        dg5 = {k: torch.from_numpy(v).cuda() for k, v in g5.items()}
+        dg5 = r.sort_gaussians_spatial({k: torch.from_numpy(v).cuda() for k, v in g5.items()})
         del g5
         acc5 = torch.zeros((H5, W5, 4), dtype=torch.float32, device="cuda")
         dep5 = torch.zeros((H5, W5), dtype=torch.float32, device="cuda")

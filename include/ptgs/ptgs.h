@@ -333,12 +333,18 @@ typedef struct ptgs_gaussians {
     const float* opacities; /* N  */
     const float* colors;    /* 3N */
     uint32_t count;
+    /* NULL, or ids[i] = the caller's index of Gaussian i (u32 N, device): a reordered copy (e.g. from
+     * ptgs_gaussians_sort_spatial) then renders exactly like the original order (sorted values, the
+     * depth tie rule and the per-Gaussian buffers use the ids) */
+    const uint32_t* ids;
 } ptgs_gaussians;
 
 typedef struct ptgs_splat_stats {
     uint32_t num_rendered; /* K = (gaussian, tile) pairs */
     uint32_t tiles_x, tiles_y;
     uint32_t num_visible;  /* gaussians with radius > 0 */
+    uint32_t fused;        /* 1: the frame ran the single-launch front end (gs_bin_fused_kernel), 0: count +
+                            * column scan + scatter */
 } ptgs_splat_stats;
 
 /* out_rgba32f (device W*H): rgb = sum c_i a_i T_i + T_final * bg, a = 1 - T_final.
@@ -369,6 +375,23 @@ int ptgs_splat_gaussians(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo*
 int ptgs_splat_gaussians_views(ptgs_ctx* ctx, const ptgs_gaussians* g, uint32_t n_views, const ptgs_ubo* ubos,
                                uint32_t width, uint32_t height, const float bg[3], float* const* outs,
                                void* hip_stream);
+
+/* Front end. Once a finished frame of the context's workspace has reported its largest tile, frames
+ * run a single-launch front end: per-tile key rows of a fixed capacity (a power of two >= 1.25x that
+ * tile, <= 8192 pairs) filled through per-tile atomic reservations, instead of the exact tile
+ * segments of count + column scan + scatter (first frame, larger tiles, PTGS_GS_FRONTEND=three).
+ * Both give the same keys, values, ranges and image. A frame with a tile above its row capacity is
+ * skipped like an over-capacity frame (counted by ptgs_splat_status_read; with stats it is re-run
+ * complete), and the next frame sizes its rows from it.
+ *
+ * Spatial order: the fused front end reserves one run per (workgroup, touched tile); Gaussians whose
+ * neighbours in memory are neighbours in space touch few tiles per workgroup. This writes a copy of
+ * g in 3D Morton order of the means (10 bits per axis over the means' bounding box, ties by index)
+ * to the caller's device buffers (sizes as g's) and ids[i] = the original index of copy i (g->ids
+ * composed when set): render the copy with .ids = ids for output identical to g's. Scene preparation
+ * (like ptgs_scene_upload's BVH build): synchronises; device temporaries are freed. */
+int ptgs_gaussians_sort_spatial(ptgs_ctx* ctx, const ptgs_gaussians* g, float* means, float* scales, float* rotations,
+                                float* opacities, float* colors, uint32_t* ids, void* hip_stream);
 
 /* Skipped-frame report of the stream-ordered splat (no stats): waits for hip_stream and the
  * context's view streams, then returns and clears the number of frames skipped since the last query
@@ -417,6 +440,9 @@ int ptgs_gaussians_from_points(ptgs_ctx* ctx, const float* xyz, const uint8_t* r
  * radii[N] (int32), tiles_touched[N] (u32), sorted keys[K] (u64: tile<<32 | depth bits),
  * sorted values[K] (u32 gaussian index), tile ranges[tiles] (uint2 start,end). sorted_keys /
  * sorted_values are NULL unless that call ran with PTGS_FLAG_SPLAT_PUBLISH and stats. */
+/* radii / tiles_touched / means2d / depths / conic_opacity are written only by frames rendered with
+ * PTGS_FLAG_SPLAT_PUBLISH (indexed by the caller's Gaussian index, see ptgs_gaussians.ids); tile_ranges
+ * by every frame (unpublished fused frames: end - begin = the tile's pair count, begin = t * capacity). */
 typedef struct ptgs_splat_buffers {
     const int32_t* radii;
     const uint32_t* tiles_touched;

@@ -136,12 +136,12 @@ class TraceStats(C.Structure):
 
 class Gaussians(C.Structure):
     _fields_ = [("means", C.c_void_p), ("scales", C.c_void_p), ("rotations", C.c_void_p),
-                ("opacities", C.c_void_p), ("colors", C.c_void_p), ("count", C.c_uint32)]
+                ("opacities", C.c_void_p), ("colors", C.c_void_p), ("count", C.c_uint32), ("ids", C.c_void_p)]
 
 
 class SplatStats(C.Structure):
     _fields_ = [("num_rendered", C.c_uint32), ("tiles_x", C.c_uint32), ("tiles_y", C.c_uint32),
-                ("num_visible", C.c_uint32)]
+                ("num_visible", C.c_uint32), ("fused", C.c_uint32)]
 
 
 class SplatStatus(C.Structure):
@@ -196,6 +196,7 @@ SYMBOLS = {
     "ptgs_splat_get_buffers": (_I, [_P, C.POINTER(SplatBuffers)]),
     "ptgs_splat_status_read": (_I, [_P, C.POINTER(SplatStatus), _P]),
     "ptgs_splat_reserve": (_I, [_P, _U]),
+    "ptgs_gaussians_sort_spatial": (_I, [_P, C.POINTER(Gaussians), _P, _P, _P, _P, _P, _P, _P]),
     "ptgs_knn3_mean_dist2": (_I, [_P, _P, _U, _P, _P]),
     "ptgs_gaussians_from_points": (_I, [_P, _P, _P, _U, _P, _P, _P, _P, _P, _P]),
     "ptgs_comm_unique_id": (_I, [_P]),

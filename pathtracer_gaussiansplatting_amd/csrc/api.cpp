@@ -606,7 +606,7 @@ static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
                         uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream) {
   if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
   if (g->count && (!is_device_ptr(g->means) || !is_device_ptr(g->scales) || !is_device_ptr(g->rotations) ||
-                   !is_device_ptr(g->opacities) || !is_device_ptr(g->colors)))
+                   !is_device_ptr(g->opacities) || !is_device_ptr(g->colors) || (g->ids && !is_device_ptr(g->ids))))
     return fail(c, PTGS_EINVAL, "gaussian arrays must be device pointers");
   if (!is_device_ptr(out)) return fail(c, PTGS_EINVAL, "out is not a device pointer");
   if ((depth && !is_device_ptr(depth)) || (under && !is_device_ptr(under)))
@@ -684,6 +684,22 @@ int ptgs_splat_gaussians_views(ptgs_ctx* c, const ptgs_gaussians* g, uint32_t n_
   const int rc = splat_common(c, g, &ubos[0], w, h, bg, nullptr, nullptr, 0, ~0u, outs[0], nullptr, stream);
   join();
   return rc;
+}
+
+int ptgs_gaussians_sort_spatial(ptgs_ctx* c, const ptgs_gaussians* g, float* means, float* scales, float* rotations,
+                                float* opacities, float* colors, uint32_t* ids, void* stream) {
+  if (!c || !g) return fail(c, PTGS_EINVAL, "null argument");
+  if (g->count) {
+    const void* all[] = {g->means, g->scales, g->rotations, g->opacities, g->colors, means, scales, rotations,
+                         opacities, colors, ids};
+    for (const void* p : all)
+      if (!is_device_ptr(p)) return fail(c, PTGS_EINVAL, "gaussian arrays must be device pointers");
+    if (g->ids && !is_device_ptr(g->ids)) return fail(c, PTGS_EINVAL, "ids must be a device pointer");
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  const hipError_t e = splat_sort_spatial(g, means, scales, rotations, opacities, colors, ids, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "ptgs_gaussians_sort_spatial: %s", hipGetErrorString(e));
+  return PTGS_OK;
 }
 
 int ptgs_splat_status_read(ptgs_ctx* c, ptgs_splat_status* out, void* stream) {

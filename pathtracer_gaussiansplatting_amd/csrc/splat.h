@@ -19,6 +19,9 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
                            ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s);
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
+// 3D Morton order of the means: a reordered copy + the original indices (synchronises s)
+hipError_t splat_sort_spatial(const ptgs_gaussians* g, float* means, float* scales, float* rots, float* opac,
+                              float* colors, uint32_t* ids, hipStream_t s);
 // grow the pair buffers to at least `pairs` (frees / reallocates: waits for the device)
 hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs);
 // frames skipped on the device (pair count above the buffer) since the last clear; the pair

@@ -19,8 +19,10 @@
 // are the bit-exact contract with oracle/ptgs_oracle.c; the image is within 1e-4 relative L2
 // (hardware exp2 in the blend).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/ptgs/ptgs.h"
@@ -55,7 +57,15 @@ struct DevBuf {
 struct SplatWorkspace {
   DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, tile_info,
       group_total, tile_slots, point_keys, total, rect, large, large_ctr, sort_scratch;
-  uint32_t* k_host = nullptr;  // pinned, coherent: the scan kernel stores K here
+  DevBuf cursor, fz, pub_offs, keys_pub, vals_pub;  // fused front end (see gs_bin_fused_kernel)
+  DevBuf dbg_depths;
+  uint32_t seq = 0;           // fused frames enqueued (the overflow word's tag)
+  bool have_hint = false;     // a finished frame has published its largest tile: the fused path can size its rows
+  bool hint_recorded = false;
+  hipEvent_t hint_event = nullptr;
+  bool last_fused = false;    // the last frame ran the fused front end
+  uint32_t* k_host = nullptr;  // pinned, coherent [8]: K, largest tile, large tiles, skipped frames,
+                               // fused reservations, fused overflow
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
@@ -73,13 +83,15 @@ void splat_workspace_destroy(SplatWorkspace* w) {
   if (!w) return;
   DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rec, &w->radii, &w->touched, &w->pairs, &w->keys_out,
                    &w->vals_out, &w->ranges, &w->hist, &w->tile_info, &w->group_total, &w->tile_slots, &w->point_keys,
-                   &w->total, &w->rect, &w->large, &w->large_ctr, &w->sort_scratch};
+                   &w->total, &w->rect, &w->large, &w->large_ctr, &w->sort_scratch, &w->cursor, &w->fz,
+                   &w->pub_offs, &w->keys_pub, &w->vals_pub, &w->dbg_depths};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
   for (hipEvent_t& e : w->ev)
     if (e) (void)hipEventDestroy(e);
   if (w->k_event) (void)hipEventDestroy(w->k_event);
+  if (w->hint_event) (void)hipEventDestroy(w->hint_event);
   delete w;
 }
 
@@ -106,19 +118,23 @@ struct PreArgs {
   const float *means, *scales, *rots, *opac, *colors;
   uint32_t n;
   float2* means2d;
-  float* depths;
+  float* depths;      // walk order (i): the three-launch scatter's depths
+  float* dbg_depths;  // caller order (o): ptgs_splat_get_buffers
   float4* conic_o;
   int* radii;
   uint32_t* touched;
   ushort4* rects;
   float4* rec;
+  const uint32_t* ids;  // caller's index of Gaussian i (NULL: i): keys, values, records and the
+                        // per-Gaussian outputs use it, so a reordered set renders like the original
 };
 
 // One Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T, EWA Sigma' = J W Sigma W^T J^T + 0.3,
 // conic, 3-sigma radius, tile rect (returned; empty if culled) and, with STORE, every per-Gaussian
 // output incl. the blend record. (Blocks of other bands recompute the rect without storing.)
 template <bool STORE>
-__device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const PreArgs& A, uint32_t i) {
+__device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const PreArgs& A, uint32_t i,
+                                                     float* dep_out = nullptr) {
   const float* __restrict__ means = A.means;
   const float* __restrict__ scales = A.scales;
   const float* __restrict__ rots = A.rots;
@@ -132,15 +148,22 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   ushort4* __restrict__ rects = A.rects;
   float4* __restrict__ rec = A.rec;
   const ushort4 none = make_ushort4(0, 0, 0, 0);
+  // per-Gaussian outputs: rec (the blend's records) always; rects / depths (the three-launch scatter's
+  // walk, at i) and radii / touched / means2d / conic (ptgs_splat_get_buffers) when their pointers are
+  // set (the fused path without PTGS_FLAG_SPLAT_PUBLISH leaves them out)
+  const uint32_t o = A.ids ? A.ids[i] : i;
   if (STORE) {
-    radii[i] = 0;
-    touched[i] = 0;
-    rects[i] = none;  // empty rect: the scatter reads rects only
+    if (radii) {
+      radii[o] = 0;
+      touched[o] = 0;
+    }
+    if (rects) rects[i] = none;  // empty rect: the scatter reads rects only
   }
   float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   // frustum: view-space depth d = -z (RH, camera looks down -Z)
   v4 pv = mv4(cam.view, mx, my, mz, 1.0f);
   float d = -pv.z;
+  if (dep_out) *dep_out = d;
   if (d <= 0.2f) return none;
   v4 ph = mv4(cam.mvp, mx, my, mz, 1.0f);
   float pw = 1.0f / (ph.w + 0.0000001f);
@@ -206,12 +229,17 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   const ushort4 rect = make_ushort4((unsigned short)rmin_x, (unsigned short)rmin_y, (unsigned short)rmax_x,
                                     (unsigned short)rmax_y);
   if (!STORE) return rect;
-  depths[i] = d;
-  radii[i] = r;
-  means2d[i] = pimg;
-  conic_o[i] = con;
-  touched[i] = (uint32_t)area;
-  rects[i] = rect;
+  if (rects) {
+    depths[i] = d;
+    rects[i] = rect;
+  }
+  if (radii) {
+    A.dbg_depths[o] = d;
+    radii[o] = r;
+    means2d[o] = pimg;
+    conic_o[o] = con;
+    touched[o] = (uint32_t)area;
+  }
   // Blend record (3 x float4), the form the blend loop consumes:
   //   (x, y, A, B), (C, log2 o, r, g), (b, ex, ey, depth)  with  A = -a/2 log2e, B = -b log2e, C = -c/2 log2e
   // so that z = A dx^2 + B dx dy + C dy^2 + log2 o = power * log2e + log2 o and alpha = min(0.99, 2^z).
@@ -222,9 +250,9 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   const float sq = -2.0f * skip;
   const float ex = sq > 0.0f ? sqrtx(sq * ca) * 1.01f + 0.01f : -1.0f;
   const float ey = sq > 0.0f ? sqrtx(sq * cc) * 1.01f + 0.01f : -1.0f;
-  rec[3 * i] = make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E);
-  rec[3 * i + 1] = make_float4(-0.5f * con.z * L2E, __log2f(con.w), colors[3 * i], colors[3 * i + 1]);
-  rec[3 * i + 2] = make_float4(colors[3 * i + 2], ex, ey, d);
+  rec[3 * o] = make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E);
+  rec[3 * o + 1] = make_float4(-0.5f * con.z * L2E, __log2f(con.w), colors[3 * i], colors[3 * i + 1]);
+  rec[3 * o + 2] = make_float4(colors[3 * i + 2], ex, ey, d);
   return rect;
 }
 
@@ -252,6 +280,7 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
 #endif
 #define GS_BAND_TILES 8192   // max tiles per band (LDS: 32 KiB count, 64 KiB scatter); W <= 131072 px
 #define GS_TILE_SLOTS 256    // fixed key slots per tile (= the register-sort limit)
+#define GS_MID 512           // tiles of (256, GS_MID] pairs are sorted inside the blend (rank counting)
 #define GS_MAX_GROUPS 4096   // 64-tile groups (262144 tiles)
 
 // Inclusive wave64 prefix sum in DPP (row_shr 1/2/4/8 inside rows of 16, then row_bcast 15 / 31
@@ -321,8 +350,8 @@ __device__ __forceinline__ void gs_clip(const ushort4& rc, uint32_t ty0, uint32_
 #define GS_WALK_PF 4
 template <typename F>
 __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* __restrict__ rects,
-                                              const float* __restrict__ depths, uint32_t n, uint32_t ty0,
-                                              uint32_t ty1, uint4* s_q, F f) {
+                                              const float* __restrict__ depths, const uint32_t* __restrict__ ids,
+                                              uint32_t n, uint32_t ty0, uint32_t ty1, uint4* s_q, F f) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t b0 = blockIdx.y * bg.chunk, b1 = min(n, b0 + bg.chunk);
   const ushort4 zero = make_ushort4(0, 0, 0, 0);
@@ -352,7 +381,7 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
       if (bal) {
         if (yh) {
           const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-          q[(head + cnt + pos) & (GS_WQ - 1u)] = make_uint4(base + lane, xw, yh, 0u);
+          q[(head + cnt + pos) & (GS_WQ - 1u)] = make_uint4(base + lane, xw, yh, ids ? ids[base + lane] : base + lane);
         }
         cnt += (uint32_t)__popcll(bal);
       }
@@ -367,7 +396,7 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
     head += take;
     cnt -= take;
     const float dep = lane < take ? depths[e.x] : 0.0f;
-    gs_expand<true>(lane, e.x, e.y, e.z, dep, f);
+    gs_expand<true>(lane, e.w, e.y, e.z, dep, f);  // (e.w: the caller's index for the key)
   }
 }
 
@@ -473,7 +502,8 @@ __global__ __launch_bounds__(GS_COLSCAN_THREADS) void gs_bin_colscan_kernel(BinG
 // (the host sizes it from the previous K and re-runs scatter + blend after growing it when it did
 // not: see splat_gaussians).
 __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
-    BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, uint32_t n,
+    BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, const uint32_t* __restrict__ ids,
+    uint32_t n,
     const uint32_t* __restrict__ hist, const uint2* __restrict__ tile_info, const uint32_t* __restrict__ group_total,
     uint32_t* __restrict__ total, const uint32_t* __restrict__ large_ctr, uint32_t* k_host, uint32_t cap,
     uint2* __restrict__ ranges,
@@ -552,12 +582,132 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
       }
       uint32_t xw, yh;
       gs_clip(rc, ty0, ty1, xw, yh);
-      if (__ballot(yh != 0u)) gs_expand<true>(lane, i, xw, yh, d, put);
+      if (__ballot(yh != 0u)) gs_expand<true>(lane, ids && i < b1 ? ids[i] : i, xw, yh, d, put);
     }
     return;
   }
 #endif
-  gs_walk_chunk(bg, rects, depths, n, ty0, ty1, s_q, put);
+  gs_walk_chunk(bg, rects, depths, ids, n, ty0, ty1, s_q, put);
+}
+
+// ---- fused front end ------------------------------------------------------------------------------
+// One launch instead of count + colscan + scatter: per-tile slot rows of a fixed capacity `scap`
+// (a power of two >= the largest tile of recent frames) replace the exact tile segments, so a tile's
+// pairs need no global prefix: block (band, c) preprocesses chunk c (one Gaussian per work-item,
+// kept in registers), counts its pairs per tile in LDS, reserves each touched tile's run with one
+// returning atomicAdd on the tile's cursor, then walks its pairs again and writes each key to
+// tile_slots[t * scap + base + LDS rank]. The order inside a row depends on the atomics' order and is
+// fixed by the per-tile sort (keys are unique), so keys / values / image equal the three-launch path.
+// The blend reads the tile's count from its cursor and zeroes it (cursors are zero between frames).
+// A tile whose count exceeds scap marks the frame (fz[2] = seq): sort and blend skip it, the host
+// counts it and falls back to the three-launch path. fz: [0] pairs, [1] largest tile above 256,
+// [2] overflow sequence, [3] reservations (atomics), published to the host by the blend.
+#ifndef GS_FUSED_THREADS
+#define GS_FUSED_THREADS 512
+#endif
+struct GsFused {  // the sort's and the blend's view of a fused-front-end frame (scap == 0: three-launch path)
+  uint32_t scap, seq;
+  uint32_t* cursor;   // per-tile pair counts (zeroed again by the blend)
+  uint32_t* fz;       // counters (see above)
+  uint32_t* k_host;   // pinned host words (published by blend block (0, 0))
+  uint2* ranges;      // the tile ranges the blend writes (t * scap, t * scap + n)
+};
+// GS_STAMP builds (tools/gs_stamps.py): per-workgroup s_memrealtime (100 MHz) stamps at phase
+// boundaries of the fused front end and the blend, read back with ptgs_debug_stamps.
+#ifdef GS_STAMP
+#define GS_STAMP_WG 65536
+#define GS_STAMP_N 8
+__device__ unsigned long long g_gs_stamps[2][GS_STAMP_WG * GS_STAMP_N];
+#define STAMP(kind, k)                                                                                      \
+  do {                                                                                                     \
+    const uint32_t wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                              \
+    if (threadIdx.x == 0 && wg_ < GS_STAMP_WG)                                                             \
+      g_gs_stamps[kind][wg_ * GS_STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime();                       \
+  } while (0)
+#define STAMP_SYNC() __syncthreads()
+#else
+#define STAMP(kind, k) do { } while (0)
+#define STAMP_SYNC() do { } while (0)
+#endif
+__global__ __launch_bounds__(GS_FUSED_THREADS) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
+                                                                         uint32_t scap, uint32_t seq,
+                                                                         uint32_t* __restrict__ cursor,
+                                                                         uint32_t* __restrict__ fz,
+                                                                         unsigned long long* __restrict__ tile_slots) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
+  __shared__ uint32_t s_red[2][GS_FUSED_THREADS / 64];
+  STAMP(0, 0);
+  uint32_t ty0, ty1;
+  gs_band(bg, ty0, ty1);
+  const uint32_t nt = (ty1 - ty0) * bg.grid_x, t0 = ty0 * bg.grid_x;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_THREADS) s_hist[k] = 0;
+  __syncthreads();
+  STAMP(0, 1);
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t i = blockIdx.y * bg.chunk + threadIdx.x;  // chunk <= GS_FUSED_THREADS (host)
+  const bool own = threadIdx.x < bg.chunk && i < A.n;
+  ushort4 rc = make_ushort4(0, 0, 0, 0);
+  const uint32_t o = own && A.ids ? A.ids[i] : i;  // the key's index (the caller's)
+  float d = 0.0f;  // view depth (every band's blocks need it for the keys; only band 0 stores it)
+  if (own) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
+  uint32_t xw, yh;
+  gs_clip(rc, ty0, ty1, xw, yh);
+  STAMP_SYNC();
+  STAMP(0, 2);
+  const bool any = __ballot(yh != 0u) != 0ull;
+  if (any)
+    gs_expand<false>(lane, i, xw, yh, 0.0f, [&](uint32_t, uint32_t x, uint32_t y, float) {
+      atomicAdd(s_hist + (y - ty0) * bg.grid_x + x, 1u);
+    });
+  __syncthreads();
+  STAMP(0, 3);
+  // reserve: one returning atomic per touched tile; the LDS entry becomes the run's base
+  uint32_t pairs = 0, res = 0;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_THREADS) {
+    const uint32_t c = s_hist[k];
+    if (c) {
+      const uint32_t base = atomicAdd(cursor + t0 + k, c);
+      s_hist[k] = base;
+      pairs += c;
+      ++res;
+      if (base + c > scap) __hip_atomic_store(fz + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (base + c > 256u) atomicMax(fz + 1, base + c);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    pairs += (uint32_t)__shfl_xor((int)pairs, off);
+    res += (uint32_t)__shfl_xor((int)res, off);
+  }
+  if (lane == 0) {
+    s_red[0][wave] = pairs;
+    s_red[1][wave] = res;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t p = 0, r = 0;
+    for (uint32_t w = 0; w < GS_FUSED_THREADS / 64; ++w) {
+      p += s_red[0][w];
+      r += s_red[1][w];
+    }
+    if (p) atomicAdd(fz, p);
+    if (r) atomicAdd(fz + 3, r);
+  }
+  STAMP(0, 4);
+#ifdef GS_STAMP
+  {
+#else
+  if (!any) return;
+#endif
+  gs_expand<true>(lane, o, xw, yh, d, [&](uint32_t g, uint32_t x, uint32_t y, float dep) {
+    const uint32_t t = y * bg.grid_x + x;
+    const uint32_t rel = atomicAdd(s_hist + (t - t0), 1u);
+    if (rel < scap) tile_slots[(size_t)t * scap + rel] = ((unsigned long long)__float_as_uint(dep) << 32) | g;
+  });
+#ifdef GS_STAMP
+  }
+  STAMP_SYNC();
+  STAMP(0, 5);
+#endif
 }
 
 // ascending bitonic sort ("flip" network: every comparator puts the min at the lower index) over
@@ -791,7 +941,7 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
     const unsigned long long* __restrict__ tile_slots, const uint32_t* __restrict__ large,
     const uint32_t* __restrict__ large_ctr, unsigned long long* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
     const uint32_t* __restrict__ total, uint32_t cap, uint32_t rmax, uint32_t* __restrict__ g_dep,
-    uint16_t* __restrict__ g_slot, uint32_t g_cap) {
+    uint16_t* __restrict__ g_slot, uint32_t g_cap, GsFused fu, uint32_t ntiles) {
   // LDS: one array per field, halves at offsets (an array of LDS pointers indexed at run time would
   // turn every access into a FLAT one)
   extern __shared__ __attribute__((aligned(16))) char s_arena[];
@@ -800,16 +950,31 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
   uint16_t* s_slot = reinterpret_cast<uint16_t*>(s_dep + 2 * capn);  // [2][capn]
   uint16_t* s_cnt = s_slot + 2 * capn;                                // [16 digits][256 work-items]
   __shared__ uint32_t s_red[2][GS_SORT_THREADS / 64];
-  if (*total > cap) return;
+  __shared__ uint32_t s_list[GS_SORT_THREADS + 1];  // fused: this block's large tiles
   const uint32_t tid = threadIdx.x;
-  const uint32_t count = large_ctr[0];
+  uint32_t count;
+  if (fu.scap) {
+    // fused front end: no tile list; block b checks tiles b, b + grid, ... (<= 256 of them: the host
+    // sizes the grid) by their cursors and sorts those above GS_MID pairs
+    if (__hip_atomic_load(fu.fz + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fu.seq) return;
+    if (tid == 0) s_list[GS_SORT_THREADS] = 0;
+    __syncthreads();
+    const uint32_t t = blockIdx.x + tid * gridDim.x;
+    if (t < ntiles && fu.cursor[t] > GS_MID) s_list[atomicAdd(&s_list[GS_SORT_THREADS], 1u)] = t;
+    __syncthreads();
+    count = s_list[GS_SORT_THREADS];
+  } else {
+    if (*total > cap) return;
+    count = large_ctr[0];
+  }
   // static striding over the list (a shared work counter serialises: ~30 ns per contended atomic,
   // 210 us for the 1M-Gaussian frame's 7k claims)
-  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
-    const uint32_t tile = large[li];
-    const uint2 range = ranges[tile];
+  for (uint32_t li = fu.scap ? 0 : blockIdx.x; li < count; li += fu.scap ? 1 : gridDim.x) {
+    const uint32_t tile = fu.scap ? s_list[li] : large[li];
+    const uint2 range = fu.scap ? make_uint2(tile * fu.scap, tile * fu.scap + fu.cursor[tile]) : ranges[tile];
     const uint32_t n = range.y - range.x;
-    unsigned long long* seg = n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
+    unsigned long long* seg = fu.scap ? const_cast<unsigned long long*>(tile_slots) + range.x
+                            : n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
                                                  : pairs + range.x;
     const uint32_t* segw = reinterpret_cast<const uint32_t*>(seg);  // (gaussian, depth) word pairs
     const unsigned long long tbits = (unsigned long long)tile << 32;
@@ -847,7 +1012,6 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
 // bitonic network: blend 70.6 -> 68.1 us at C2 (kernel trace; 128: 67.8, within noise)
 #define GS_SMALL_RANK 256
 #endif
-#define GS_MID 512  // tiles of (256, GS_MID] pairs are sorted inside the blend (rank counting)
 
 struct GStage {  // one staged blend record (see gs_preprocess_one)
   float4 a, b, c;
@@ -889,7 +1053,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
                                                                  const unsigned long long* __restrict__ tile_slots,
                                                                  const float* __restrict__ depth_lim,
                                                                  const float4* __restrict__ under,
-                                                                 float4* __restrict__ out) {
+                                                                 float4* __restrict__ out, GsFused fu) {
   // staged records of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads the
   // per-quadrant lists to a multiple of 4.
   __shared__ __attribute__((aligned(16))) char s_arena[GS_ARENA];
@@ -900,8 +1064,32 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   unsigned long long* s_key = reinterpret_cast<unsigned long long*>(s_arena);
   __shared__ uint8_t s_mask[GS_BLOCK];
   __shared__ uint8_t s_sslot[GS_BLOCK];  // small tiles: staging slot of sorted position p
-  if (*total > cap) return;  // pair buffer too small this frame: the host re-runs after growing it
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+  STAMP(1, 0);
+  if (fu.scap) {
+    // fused front end: block (0, 0) hands the frame's counters to the host and re-arms them (the
+    // fused kernel that produced them has finished; no other blend block reads them)
+    const bool ovf = __hip_atomic_load(fu.fz + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fu.seq;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
+      const uint32_t big = fu.fz[1];
+      __atomic_store_n(fu.k_host + 1, big > 256u ? big : 256u, __ATOMIC_RELAXED);  // largest tile (bound)
+      __atomic_store_n(fu.k_host + 2, 0u, __ATOMIC_RELAXED);
+      __atomic_store_n(fu.k_host + 4, fu.fz[3], __ATOMIC_RELAXED);                  // reservations
+      __atomic_store_n(fu.k_host + 5, ovf ? 1u : 0u, __ATOMIC_RELAXED);            // tile above scap
+      if (ovf) __atomic_store_n(fu.k_host + 3, __atomic_load_n(fu.k_host + 3, __ATOMIC_RELAXED) + 1u, __ATOMIC_RELAXED);
+      __atomic_store_n(fu.k_host, fu.fz[0], __ATOMIC_RELAXED);
+      fu.fz[0] = 0;
+      fu.fz[1] = 0;
+      fu.fz[3] = 0;
+      __threadfence_system();
+    }
+    if (ovf) {  // a tile did not fit its row: the frame is skipped (counted); cursors re-armed
+      if (tid == 0) fu.cursor[(cam.row_begin + blockIdx.y) * cam.grid_x + blockIdx.x] = 0;
+      return;
+    }
+  } else if (*total > cap) {
+    return;  // pair buffer too small this frame: the host re-runs after growing it
+  }
 #if GS_XCD_REMAP
   // XCD-aware: the workgroups of one XCD blend one horizontal strip of tiles, so the records of the
   // Gaussians they share stay in that XCD's L2
@@ -937,11 +1125,19 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   const uint32_t n = range.y - range.x;
   const unsigned long long k_slot = tid < n ? tile_slots[(size_t)tile * GS_TILE_SLOTS + tid] : ~0ull;
 #else
-  const unsigned long long k_slot = tile_slots[(size_t)tile * GS_TILE_SLOTS + tid];
-  const uint2 range = ranges[tile];
+  const uint32_t srow = fu.scap ? fu.scap : GS_TILE_SLOTS;
+  const unsigned long long k_slot = tile_slots[(size_t)tile * srow + tid];
+  uint2 range;
+  if (fu.scap) {
+    const uint32_t c = fu.cursor[tile];
+    range = make_uint2(tile * fu.scap, tile * fu.scap + c);
+  } else {
+    range = ranges[tile];
+  }
   const uint32_t n = range.y - range.x;
 #endif
   const bool small = slot_keys && n <= GS_BLOCK;
+  if (fu.scap && tid == 0) fu.ranges[tile] = range;
   const bool mid = !small && n <= sorted_above;  // not sorted by gs_sort_large_kernel: sorted here
   const bool mid_lds = mid && n <= GS_MID;
   const unsigned long long tbits = (unsigned long long)tile << 32;
@@ -1022,7 +1218,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
    }
   } else {
     if (mid) {
-      unsigned long long* seg = n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
+      unsigned long long* seg = fu.scap ? const_cast<unsigned long long*>(tile_slots) + range.x
+                              : n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
                                                    : pairs + range.x;
       if (mid_lds) {
         // rank by counting (keys are unique: the gaussian is in the low word): each work-item ranks
@@ -1088,6 +1285,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
   const char* stage = reinterpret_cast<const char*>(s_stage);
   int todo = (int)n;
+  STAMP(1, 1);
   for (uint32_t base = 0; todo > 0; base += GS_BLOCK, todo -= GS_BLOCK) {
     // (small tiles: the barrier also publishes the records, masks and sorted slots staged after the
     // sort; large tiles: every wave is done with the previous batch)
@@ -1171,6 +1369,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       }
     }
   }
+  STAMP(1, 2);
+  if (fu.scap && tid == 0 && n) fu.cursor[tile] = 0;  // (n > 0: every wave passed a barrier after reading it)
   if (inside) {
     // the pixel index is recomputed here from a laundered thread id, so that the one computed before
     // the batch loop is not kept (spilled) across it
@@ -1186,7 +1386,51 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       out[pix] = make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T);
     }
   }
+  STAMP_SYNC();
+  STAMP(1, 3);
 #endif
+}
+
+// Published frame of the fused front end (PTGS_FLAG_SPLAT_PUBLISH, tests): the blend wrote each tile's
+// sorted keys / values at t * scap; these two launches compact them into the three-launch layout
+// (exclusive scan of the tile counts -> ranges, empty tiles (0, 0)) so both paths publish alike.
+// Unpublished fused frames leave ranges[t] = (t * scap, t * scap + n): end - begin is the count.
+#define GS_PUB_THREADS 1024
+__global__ __launch_bounds__(GS_PUB_THREADS) void gs_publish_scan_kernel(const uint2* __restrict__ fr, uint32_t ntiles,
+                                                                         uint32_t t_begin, uint32_t t_end,
+                                                                         uint32_t* __restrict__ offs) {
+  __shared__ uint32_t s_part[GS_PUB_THREADS / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t per = (ntiles + GS_PUB_THREADS - 1) / GS_PUB_THREADS, a = tid * per, b = min(ntiles, a + per);
+  uint32_t sum = 0;
+  for (uint32_t t = a; t < b; ++t) sum += (t >= t_begin && t < t_end) ? fr[t].y - fr[t].x : 0u;
+  const uint32_t incl = wave_incl_scan(sum);
+  if (lane == 63) s_part[wv] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+  for (uint32_t w = 0; w < wv; ++w) run += s_part[w];
+  for (uint32_t t = a; t < b; ++t) {
+    offs[t] = run;
+    run += (t >= t_begin && t < t_end) ? fr[t].y - fr[t].x : 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void gs_publish_copy_kernel(const uint2* __restrict__ fr, const uint32_t* __restrict__ offs,
+                                                              uint32_t t_begin, uint32_t t_end,
+                                                              const unsigned long long* __restrict__ keys_in,
+                                                              const uint32_t* __restrict__ vals_in,
+                                                              unsigned long long* __restrict__ keys_out,
+                                                              uint32_t* __restrict__ vals_out, uint2* __restrict__ ranges) {
+  const uint32_t t = blockIdx.x;
+  const bool in = t >= t_begin && t < t_end;
+  const uint2 r = in ? fr[t] : make_uint2(0u, 0u);
+  const uint32_t n = r.y - r.x, o = offs[t];
+  __syncthreads();  // (ranges may be fr itself: every work-item has read fr[t])
+  if (threadIdx.x == 0) ranges[t] = n ? make_uint2(o, o + n) : make_uint2(0u, 0u);
+  for (uint32_t k = threadIdx.x; k < n; k += 256) {
+    keys_out[o + k] = keys_in[r.x + k];
+    vals_out[o + k] = vals_in[r.x + k];
+  }
 }
 
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
@@ -1220,6 +1464,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   if ((e = ensure(w->conic, (size_t)n * 16))) return e;
   if ((e = ensure(w->rec, (size_t)n * 48))) return e;
   if ((e = ensure(w->radii, (size_t)n * 4))) return e;
+  if ((e = ensure(w->dbg_depths, (size_t)n * 4))) return e;
   if ((e = ensure(w->touched, (size_t)n * 4))) return e;
   if ((e = ensure(w->rect, (size_t)n * 8))) return e;
   if ((e = ensure(w->ranges, (size_t)tiles * 8))) return e;
@@ -1252,8 +1497,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = hipMemset(w->total.p, 0, 16))) return e;
   }
   if (!w->k_host) {
-    if ((e = hipHostMalloc((void**)&w->k_host, 16, hipHostMallocCoherent | hipHostMallocMapped))) return e;
-    std::memset(w->k_host, 0, 16);
+    if ((e = hipHostMalloc((void**)&w->k_host, 32, hipHostMallocCoherent | hipHostMallocMapped))) return e;
+    std::memset(w->k_host, 0, 32);
     if ((e = hipHostGetDevicePointer((void**)&w->k_dev, w->k_host, 0))) return e;
   }
 #ifndef GS_K_EVENT_FLAGS
@@ -1301,25 +1546,119 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   pa.touched = (uint32_t*)w->touched.p;
   pa.rects = (ushort4*)w->rect.p;
   pa.rec = (float4*)w->rec.p;
-  if ((e = mark(0))) return e;
-  // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
-  hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_COUNT_THREADS), band_lds, s, cam, pa,
-                     bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev);
-  if ((e = hipGetLastError())) return e;
-  if ((e = mark(1))) return e;
-  hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(GS_COLSCAN_THREADS), 0, s, bgrid, (uint32_t*)w->hist.p,
-                     (uint2*)w->tile_info.p, (uint32_t*)w->group_total.p, (uint32_t*)w->total.p, (uint32_t)GS_MID,
-                     (uint32_t*)w->large.p, (uint32_t*)w->large_ctr.p);
-  if ((e = hipGetLastError())) return e;
-  if ((e = mark(2))) return e;
-
+  pa.ids = g->ids;
+  pa.dbg_depths = (float*)w->dbg_depths.p;
+  if (!publish) {  // the per-Gaussian debug outputs only for a published frame (ptgs_splat_get_buffers)
+    pa.radii = nullptr;
+    pa.touched = nullptr;
+    pa.means2d = nullptr;
+    pa.conic_o = nullptr;
+    pa.dbg_depths = nullptr;
+  }
+  // Front end: the fused single launch (gs_bin_fused_kernel) once an earlier frame of this workspace
+  // has published its largest tile (the rows' capacity scap follows it with 1/4 headroom, a power of
+  // two in [256, GS_FUSED_MAX_SCAP]); otherwise, or above that capacity, count + colscan + scatter.
+#ifndef GS_FUSED_MAX_SCAP
+#define GS_FUSED_MAX_SCAP 8192u
+#endif
+#ifndef GS_FRONTEND_DEFAULT
+#define GS_FRONTEND_DEFAULT 1  // 0: always three launches
+#endif
+  static const int frontend = [] {
+    const char* v = getenv("PTGS_GS_FRONTEND");  // "fused" / "three" (A/B switch)
+    if (v && !strcmp(v, "three")) return 0;
+    if (v && !strcmp(v, "fused")) return 1;
+    return GS_FRONTEND_DEFAULT;
+  }();
+  uint32_t scap = 0;
+  if (frontend && w->have_hint && n) {
+    const uint32_t big = std::max(256u, w->k_host[1] + w->k_host[1] / 4u);
+    uint32_t c = 256;
+    while (c < big && c < GS_FUSED_MAX_SCAP) c <<= 1;
+    if (big <= GS_FUSED_MAX_SCAP && (size_t)tiles * c * 8 <= ((size_t)4 << 30)) scap = c;
+  }
   const uint32_t rows = cam.row_end - cam.row_begin;
+  auto blend = [&](uint32_t cap, const GsFused& fu, unsigned long long* keys_out, bool sort_large) -> hipError_t {
+    if (rows == 0) return hipSuccess;
+    auto k = depth ? gs_sort_blend_kernel<true> : gs_sort_blend_kernel<false>;
+    const dim3 grid(cam.grid_x, rows);
+    hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
+                       sort_large ? (uint32_t)GS_MID : 0xFFFFFFFFu, keys_out, (uint32_t*)w->vals_out.p,
+                       (const float4*)w->rec.p, bg[0], bg[1], bg[2], (const uint32_t*)w->total.p, cap, slot_keys,
+                       (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out, fu);
+    return hipGetLastError();
+  };
+  auto sort_attr = [&]() -> hipError_t {
+    if (w->sort_attr) return hipSuccess;
+    hipError_t e2 = hipFuncSetAttribute((const void*)gs_sort_large_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)gs_radix_lds(GS_RADIX_MAXR));
+    if (!e2) w->sort_attr = true;
+    return e2;
+  };
+  const GsFused no_fu = {0u, 0u, nullptr, nullptr, nullptr, nullptr};
+
+  auto enqueue_fused = [&]() -> hipError_t {
+    hipError_t e2;
+    if ((e2 = ensure(w->tile_slots, (size_t)tiles * scap * 8))) return e2;
+    if ((e2 = ensure(w->vals_out, (size_t)tiles * scap * 4))) return e2;
+    if (publish && (e2 = ensure(w->keys_out, (size_t)tiles * scap * 8))) return e2;
+    if (w->cursor.bytes < (size_t)tiles * 4) {  // zero between frames (the blend re-arms what it reads)
+      if ((e2 = ensure(w->cursor, (size_t)tiles * 4))) return e2;
+      if ((e2 = hipMemsetAsync(w->cursor.p, 0, w->cursor.bytes, s))) return e2;
+    }
+    if (!w->fz.p) {
+      if ((e2 = ensure(w->fz, 64))) return e2;
+      if ((e2 = hipMemsetAsync(w->fz.p, 0, 64, s))) return e2;
+    }
+    const uint32_t seq = ++w->seq;
+    GsFused fu = {scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p};
+    PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers
+    fpa.rects = nullptr;
+    fpa.depths = nullptr;
+    BinGrid fg = bgrid;
+    fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
+    fg.chunk = GS_FUSED_THREADS;
+    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks), dim3(GS_FUSED_THREADS), band_lds, s, cam, fpa, fg,
+                       scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (unsigned long long*)w->tile_slots.p);
+    if ((e2 = hipGetLastError())) return e2;
+    if ((e2 = mark(1)) || (e2 = mark(2)) || (e2 = mark(3))) return e2;
+    unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
+    const bool sort_large = w->k_host[1] > GS_MID;
+    if (sort_large) {
+      if ((e2 = sort_attr())) return e2;
+      const uint32_t grid = std::max(w->sort_grid, (tiles + GS_SORT_THREADS - 1) / GS_SORT_THREADS);
+      hipLaunchKernelGGL(gs_sort_large_kernel, dim3(grid), dim3(GS_SORT_THREADS), gs_radix_lds(w->sort_r), s,
+                         (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
+                         (const unsigned long long*)w->tile_slots.p, (const uint32_t*)w->large.p,
+                         (const uint32_t*)w->large_ctr.p, keys_out, (uint32_t*)w->vals_out.p,
+                         (const uint32_t*)w->total.p, 0u, w->sort_r, (uint32_t*)nullptr, (uint16_t*)nullptr, 0u, fu, tiles);
+      if ((e2 = hipGetLastError())) return e2;
+    }
+    if ((e2 = mark(4)) || (e2 = mark(5))) return e2;
+    if ((e2 = blend(0u, fu, keys_out, sort_large))) return e2;
+    if (publish) {  // compact the published rows into the three-launch layout (tests only)
+      if ((e2 = ensure(w->pub_offs, (size_t)tiles * 4))) return e2;
+      if ((e2 = ensure(w->keys_pub, (size_t)tiles * scap * 8))) return e2;  // (K <= tiles * scap)
+      if ((e2 = ensure(w->vals_pub, (size_t)tiles * scap * 4))) return e2;
+      const uint32_t tb = cam.row_begin * cam.grid_x, te = cam.row_end * cam.grid_x;
+      hipLaunchKernelGGL(gs_publish_scan_kernel, dim3(1), dim3(GS_PUB_THREADS), 0, s, (const uint2*)w->ranges.p, tiles,
+                         tb, te, (uint32_t*)w->pub_offs.p);
+      hipLaunchKernelGGL(gs_publish_copy_kernel, dim3(tiles), dim3(256), 0, s, (const uint2*)w->ranges.p,
+                         (const uint32_t*)w->pub_offs.p, tb, te, (const unsigned long long*)w->keys_out.p,
+                         (const uint32_t*)w->vals_out.p, (unsigned long long*)w->keys_pub.p, (uint32_t*)w->vals_pub.p,
+                         (uint2*)w->ranges.p);
+      if ((e2 = hipGetLastError())) return e2;
+    }
+    if (stats && (e2 = hipEventRecord(w->k_event, s))) return e2;  // K is on the host after the blend
+    return mark(6);
+  };
+
   auto enqueue_tail = [&](uint32_t cap) -> hipError_t {
     // (read here, not before: grow() may have moved the published-keys buffer since the last call)
     unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
     hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS),
                        2 * band_lds + (size_t)bgrid.groups * 4, s, bgrid, (const ushort4*)w->rect.p,
-                       (const float*)w->depths.p, n, (const uint32_t*)w->hist.p, (const uint2*)w->tile_info.p,
+                       (const float*)w->depths.p, g->ids, n, (const uint32_t*)w->hist.p, (const uint2*)w->tile_info.p,
                        (const uint32_t*)w->group_total.p, (uint32_t*)w->total.p, (const uint32_t*)w->large_ctr.p, w->k_dev, cap,
                        (uint2*)w->ranges.p, (unsigned long long*)w->pairs.p, (unsigned long long*)w->tile_slots.p);
     hipError_t e2 = hipGetLastError();
@@ -1330,12 +1669,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     // the blend sorts the rare one itself)
     const bool sort_large = w->k_host[1] > GS_MID;
     if (sort_large) {
-      if (!w->sort_attr) {
-        if ((e2 = hipFuncSetAttribute((const void*)gs_sort_large_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)gs_radix_lds(GS_RADIX_MAXR))))
-          return e2;
-        w->sort_attr = true;
-      }
+      if ((e2 = sort_attr())) return e2;
       // tiles beyond the LDS capacity sort in a global scratch ([2][g_cap] u32 + [2][g_cap] u16 at the
       // pair offsets), allocated once a frame has had such tiles
       uint32_t g_cap = 0;
@@ -1349,31 +1683,49 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                          (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
                          (const unsigned long long*)w->tile_slots.p, (const uint32_t*)w->large.p,
                          (const uint32_t*)w->large_ctr.p, keys_out, (uint32_t*)w->vals_out.p,
-                         (const uint32_t*)w->total.p, cap, w->sort_r, g_dep, g_slot, g_cap);
+                         (const uint32_t*)w->total.p, cap, w->sort_r, g_dep, g_slot, g_cap, no_fu, tiles);
       if ((e2 = hipGetLastError())) return e2;
     }
-    if ((e2 = mark(4))) return e2;
-    if ((e2 = mark(5))) return e2;
-    if (rows > 0) {
-      auto k = depth ? gs_sort_blend_kernel<true> : gs_sort_blend_kernel<false>;
-      const dim3 grid(cam.grid_x, rows);
-      hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p,
-                         (unsigned long long*)w->pairs.p, sort_large ? (uint32_t)GS_MID : 0xFFFFFFFFu,
-                         keys_out, (uint32_t*)w->vals_out.p, (const float4*)w->rec.p,
-                         bg[0], bg[1], bg[2], (const uint32_t*)w->total.p, cap, slot_keys,
-                         (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out);
-      if ((e2 = hipGetLastError())) return e2;
-    }
+    if ((e2 = mark(4)) || (e2 = mark(5))) return e2;
+    if ((e2 = blend(cap, no_fu, keys_out, sort_large))) return e2;
     return mark(6);
   };
-  if ((e = enqueue_tail(cap_now()))) return e;
+  auto enqueue_three = [&]() -> hipError_t {
+    hipError_t e2;
+    if ((e2 = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e2;
+    // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
+    hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_COUNT_THREADS), band_lds, s, cam, pa,
+                       bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev);
+    if ((e2 = hipGetLastError())) return e2;
+    if ((e2 = mark(1))) return e2;
+    hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(GS_COLSCAN_THREADS), 0, s, bgrid, (uint32_t*)w->hist.p,
+                       (uint2*)w->tile_info.p, (uint32_t*)w->group_total.p, (uint32_t*)w->total.p, (uint32_t)GS_MID,
+                       (uint32_t*)w->large.p, (uint32_t*)w->large_ctr.p);
+    if ((e2 = hipGetLastError())) return e2;
+    if ((e2 = mark(2))) return e2;
+    return enqueue_tail(cap_now());
+  };
+
+  if ((e = mark(0))) return e;
+  const bool fused = scap != 0;
+  if ((e = fused ? enqueue_fused() : enqueue_three())) return e;
   uint32_t K = w->k_host[0];  // without stats: the latest K any frame published (a hint)
+  bool redone = false;
   if (stats) {
     if ((e = hipEventSynchronize(w->k_event))) return e;
     K = w->k_host[0];
-    if (K > cap_now()) {  // did not fit: grow and re-run scatter, sort and blend
-      // (the device counted the skipped attempt; this frame will be complete: uncount it. Every
-      // earlier frame of this workspace has finished, so no device write of the word is pending)
+    // a fused frame with a tile above its row capacity, or a three-launch frame above the pair
+    // buffer, was skipped on the device (and counted): this call re-runs it so that it is complete
+    // (uncounted again: every earlier frame of this workspace has finished, so no device write of
+    // the word is pending)
+    if (fused && w->k_host[5]) {
+      if (w->k_host[3]) w->k_host[3] -= 1u;
+      redone = true;
+      if ((e = mark(0)) || (e = enqueue_three())) return e;
+      if ((e = hipEventSynchronize(w->k_event))) return e;
+      K = w->k_host[0];
+    }
+    if ((!fused || redone) && K > cap_now()) {
       if (w->k_host[3]) w->k_host[3] -= 1u;
       if ((e = grow(K))) return e;
       if ((e = mark(2))) return e;
@@ -1383,6 +1735,19 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     stats->tiles_x = cam.grid_x;
     stats->tiles_y = cam.grid_y;
     stats->num_visible = 0;
+    stats->fused = fused && !redone ? 1u : 0u;
+  }
+  w->last_fused = fused && !redone;
+  // the fused path sizes its rows from the largest tile of a finished frame: valid once the host has
+  // seen one complete (a frame still in flight has not written its hint yet)
+  if (!w->have_hint) {
+    if (!w->hint_event && (e = hipEventCreateWithFlags(&w->hint_event, hipEventDisableTiming))) return e;
+    if (w->hint_recorded && hipEventQuery(w->hint_event) == hipSuccess) w->have_hint = true;
+    if (!w->hint_recorded || stats) {
+      if ((e = hipEventRecord(w->hint_event, s))) return e;
+      w->hint_recorded = true;
+    }
+    if (stats) w->have_hint = true;  // (waited for above)
   }
   {  // the next frame's large-tile sort: LDS capacity from the largest tile of a recent frame
      // (k_host[1]; +1/8 headroom), workgroups from its large-tile count (k_host[2]); hints only
@@ -1395,6 +1760,103 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   w->last_tiles = tiles;
   w->last_published = publish && stats;
   return hipSuccess;
+}
+
+// ---- spatial order (ptgs_gaussians_sort_spatial) ---------------------------------------------------
+__device__ __forceinline__ uint32_t gs_f2ord(float f) {  // order-preserving float -> uint
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float gs_ord2f(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u); }
+__device__ __forceinline__ uint32_t gs_spread3(uint32_t v) {  // 10 bits -> every 3rd bit
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+
+__global__ __launch_bounds__(256) void gs_means_bounds_kernel(const float* __restrict__ means, uint32_t n,
+                                                              uint32_t* __restrict__ b) {  // b: lo[3], hi[3]
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  if (i < n)
+    for (int a = 0; a < 3; ++a) lo[a] = hi[a] = means[3 * i + a];
+  for (int off = 32; off > 0; off >>= 1)
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
+      hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
+    }
+  if ((threadIdx.x & 63u) == 0)
+    for (int a = 0; a < 3; ++a) {
+      atomicMin(b + a, gs_f2ord(lo[a]));
+      atomicMax(b + 3 + a, gs_f2ord(hi[a]));
+    }
+}
+
+__global__ __launch_bounds__(256) void gs_means_morton_kernel(const float* __restrict__ means, uint32_t n,
+                                                              const uint32_t* __restrict__ b,
+                                                              unsigned long long* __restrict__ keys) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  uint32_t q[3];
+  for (int a = 0; a < 3; ++a) {
+    const float lo = gs_ord2f(b[a]), ext = gs_ord2f(b[3 + a]) - lo;
+    const float u = ext > 0.0f ? (means[3 * i + a] - lo) / ext : 0.0f;
+    q[a] = (uint32_t)fminf(fmaxf(u * 1024.0f, 0.0f), 1023.0f);
+  }
+  const uint32_t code = (gs_spread3(q[0]) << 2) | (gs_spread3(q[1]) << 1) | gs_spread3(q[2]);
+  keys[i] = ((unsigned long long)code << 32) | i;
+}
+
+__global__ __launch_bounds__(256) void gs_gather_sorted_kernel(const unsigned long long* __restrict__ keys, uint32_t n,
+                                                               ptgs_gaussians g, float* __restrict__ means,
+                                                               float* __restrict__ scales, float* __restrict__ rots,
+                                                               float* __restrict__ opac, float* __restrict__ colors,
+                                                               uint32_t* __restrict__ ids) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = (uint32_t)keys[i];
+  for (int a = 0; a < 3; ++a) {
+    means[3 * i + a] = g.means[3 * j + a];
+    scales[3 * i + a] = g.scales[3 * j + a];
+    colors[3 * i + a] = g.colors[3 * j + a];
+  }
+  for (int a = 0; a < 4; ++a) rots[4 * i + a] = g.rotations[4 * j + a];
+  opac[i] = g.opacities[j];
+  ids[i] = g.ids ? g.ids[j] : j;
+}
+
+hipError_t splat_sort_spatial(const ptgs_gaussians* g, float* means, float* scales, float* rots, float* opac,
+                              float* colors, uint32_t* ids, hipStream_t s) {
+  const uint32_t n = g->count;
+  if (n == 0) return hipSuccess;
+  hipError_t e;
+  uint32_t* b = nullptr;
+  unsigned long long *k0 = nullptr, *k1 = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+  const dim3 grid((n + 255) / 256);
+  auto done = [&](hipError_t r) {
+    (void)hipStreamSynchronize(s);
+    if (b) (void)hipFree(b);
+    if (k0) (void)hipFree(k0);
+    if (k1) (void)hipFree(k1);
+    if (tmp) (void)hipFree(tmp);
+    return r;
+  };
+  if ((e = hipMalloc(&b, 32)) || (e = hipMalloc(&k0, (size_t)n * 8)) || (e = hipMalloc(&k1, (size_t)n * 8))) return done(e);
+  if ((e = hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, k0, k1, (int)n, 0, 62, s))) return done(e);
+  if ((e = hipMalloc(&tmp, tmp_bytes))) return done(e);
+  if ((e = hipMemcpyAsync(b, init, sizeof(init), hipMemcpyHostToDevice, s))) return done(e);
+  hipLaunchKernelGGL(gs_means_bounds_kernel, grid, dim3(256), 0, s, g->means, n, b);
+  hipLaunchKernelGGL(gs_means_morton_kernel, grid, dim3(256), 0, s, g->means, n, (const uint32_t*)b, k0);
+  if ((e = hipGetLastError())) return done(e);
+  if ((e = hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, k0, k1, (int)n, 0, 62, s))) return done(e);
+  hipLaunchKernelGGL(gs_gather_sorted_kernel, grid, dim3(256), 0, s, (const unsigned long long*)k1, n, *g, means, scales,
+                     rots, opac, colors, ids);
+  return done(hipGetLastError());
 }
 
 hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs) {
@@ -1428,11 +1890,11 @@ hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms) {
 void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out) {
   out->radii = (const int32_t*)w->radii.p;
   out->tiles_touched = (const uint32_t*)w->touched.p;
-  out->sorted_keys = w->last_published ? (const uint64_t*)w->keys_out.p : nullptr;
-  out->sorted_values = w->last_published ? (const uint32_t*)w->vals_out.p : nullptr;
+  out->sorted_keys = !w->last_published ? nullptr : (const uint64_t*)(w->last_fused ? w->keys_pub.p : w->keys_out.p);
+  out->sorted_values = !w->last_published ? nullptr : (const uint32_t*)(w->last_fused ? w->vals_pub.p : w->vals_out.p);
   out->tile_ranges = (const uint32_t*)w->ranges.p;
   out->means2d = (const float*)w->means2d.p;
-  out->depths = (const float*)w->depths.p;
+  out->depths = (const float*)w->dbg_depths.p;
   out->conic_opacity = (const float*)w->conic.p;
   out->num_gaussians = w->last_n;
   out->num_rendered = w->last_k;
@@ -1446,3 +1908,12 @@ hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long**
 }
 
 }  // namespace ptgs
+
+#ifdef GS_STAMP
+extern "C" int ptgs_debug_stamps(int kind, unsigned long long* host, unsigned int n) {
+  const size_t per = sizeof(ptgs::g_gs_stamps[0]);
+  if (n * 8ull > per) n = (unsigned int)(per / 8);
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ptgs::g_gs_stamps), (size_t)n * 8, (size_t)kind * per,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

@@ -33,6 +33,16 @@ def _ptr(x) -> int:
     raise TypeError(f"cannot take a device pointer of {type(x)}")
 
 
+def _gaussians(g: dict) -> Gaussians:
+    """ptgs_gaussians of a dict of device tensors (means, scales, rotations, opacities, colors[, ids])."""
+    gs = Gaussians()
+    gs.means, gs.scales, gs.rotations = _ptr(g["means"]), _ptr(g["scales"]), _ptr(g["rotations"])
+    gs.opacities, gs.colors = _ptr(g["opacities"]), _ptr(g["colors"])
+    gs.count = int(g["means"].shape[0])
+    gs.ids = _ptr(g.get("ids"))
+    return gs
+
+
 def _stream(stream) -> int:
     if stream is None:
         try:
@@ -201,10 +211,7 @@ class Renderer:
                         tile_rows: tuple | None = None, want_stats: bool = False, stream=None, over=None):
         """over=(depth, under): the hybrid composite of ptgs_splat_gaussians_over (device depth[H, W],
         under RGBA32F[H, W, 4]; out may be under itself)."""
-        gs = Gaussians()
-        gs.means, gs.scales, gs.rotations = _ptr(g["means"]), _ptr(g["scales"]), _ptr(g["rotations"])
-        gs.opacities, gs.colors = _ptr(g["opacities"]), _ptr(g["colors"])
-        gs.count = int(g["means"].shape[0])
+        gs = _gaussians(g)
         bgc = np.asarray(bg, np.float32)
         t0, t1 = (0, 0xFFFFFFFF) if tile_rows is None else tile_rows
         st = SplatStats()
@@ -225,16 +232,27 @@ class Renderer:
         n = len(ubos)
         if len(outs) != n:
             raise ValueError("one output per view")
-        gs = Gaussians()
-        gs.means, gs.scales, gs.rotations = _ptr(g["means"]), _ptr(g["scales"]), _ptr(g["rotations"])
-        gs.opacities, gs.colors = _ptr(g["opacities"]), _ptr(g["colors"])
-        gs.count = int(g["means"].shape[0])
+        gs = _gaussians(g)
         bgc = np.asarray(bg, np.float32)
         arr = (Ubo * n)(*ubos)
         optrs = (C.c_void_p * n)(*[_ptr(o) for o in outs])
         rc = self.lib.ptgs_splat_gaussians_views(self._h, C.byref(gs), n, arr, width, height, _abi.fptr(bgc), optrs,
                                                  _stream(stream))
         self._chk(rc, "ptgs_splat_gaussians_views")
+
+    def sort_gaussians_spatial(self, g: dict, stream=None) -> dict:
+        """ptgs_gaussians_sort_spatial: a copy of the device Gaussians `g` in 3D Morton order of the means
+        plus "ids" (int32 tensor: the original index of each copy); splatting the copy renders exactly like
+        `g` (scene preparation: synchronises)."""
+        import torch
+        out = {k: torch.empty_like(g[k]) for k in ("means", "scales", "rotations", "opacities", "colors")}
+        n = int(g["means"].shape[0])
+        out["ids"] = torch.empty(n, dtype=torch.int32, device=g["means"].device)
+        rc = self.lib.ptgs_gaussians_sort_spatial(self._h, C.byref(_gaussians(g)), _ptr(out["means"]), _ptr(out["scales"]),
+                                                  _ptr(out["rotations"]), _ptr(out["opacities"]), _ptr(out["colors"]),
+                                                  _ptr(out["ids"]), _stream(stream))
+        self._chk(rc, "ptgs_gaussians_sort_spatial")
+        return out
 
     def splat_status(self, stream=None) -> SplatStatus:
         """ptgs_splat_status_read: waits for `stream` and the view streams, returns and clears the

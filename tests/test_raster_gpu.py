@@ -323,6 +323,115 @@ def test_gaussians_stream_ordered_graph_replay(renderer, oracle_lib):
     del graph
 
 
+def _check_published(r, st, ref, out, n, what):
+    b = r.splat_buffers()
+    assert st.num_rendered == ref["K"], what
+    np.testing.assert_array_equal(_read(r, b.sorted_keys, ref["K"], np.uint64), ref["keys"], err_msg=what)
+    np.testing.assert_array_equal(_read(r, b.sorted_values, ref["K"], np.uint32), ref["vals"], err_msg=what)
+    np.testing.assert_array_equal(_read(r, b.tile_ranges, 2 * b.num_tiles, np.uint32), ref["ranges"], err_msg=what)
+    np.testing.assert_array_equal(_read(r, b.radii, n, np.int32), ref["radii"], err_msg=what)
+    np.testing.assert_array_equal(_read(r, b.tiles_touched, n, np.uint32), ref["touched"], err_msg=what)
+    err = U.rel_l2(out.cpu().numpy(), ref["image"])
+    assert err < 1e-4, (what, err)
+
+
+@pytest.mark.parametrize("n,W,H", [(100_000, 1920, 1080),  # C2
+                                   (20_000, 320, 180),     # tiles of 256-1000 pairs (in-blend and radix sorts)
+                                   (3000, 3840, 2160)])    # 4K: four bands of tile rows
+def test_gaussians_fused_front_end(native_lib, oracle_lib, n, W, H):
+    """The single-launch front end (per-tile rows filled through atomic reservations) runs from the
+    second frame of a context on: its sorted keys / values / ranges, radii / tiles touched (bit-exact)
+    and image (< 1e-4) equal the oracle's, as the first (three-launch) frame's do."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    g = Y.gaussians_c2(n, seed=9)
+    g["means"][1::53] = g["means"][0::53][: len(g["means"][1::53])]  # duplicated means: equal depths
+    ubo = _gauss_ubo(W, H)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H, bg=(0.1, 0.2, 0.3))
+    r = Renderer(0, publish_splat_buffers=True)
+    try:
+        dg = {k: _dev(v) for k, v in g.items()}
+        for frame in range(3):
+            out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            st = r.splat_gaussians(dg, ubo, W, H, out, bg=(0.1, 0.2, 0.3), want_stats=True)
+            torch.cuda.synchronize()
+            assert st.fused == (frame > 0), (frame, st.fused)
+            _check_published(r, st, ref, out, n, f"frame {frame}")
+    finally:
+        r.close()
+
+
+def test_gaussians_spatial_order_renders_identically(native_lib, oracle_lib):
+    """ptgs_gaussians_sort_spatial: the Morton-ordered copy with its ids renders the original set's
+    frame exactly - sorted keys / values (the caller's indices, equal depths in index order), ranges,
+    radii / tiles touched by the caller's index - through both front ends, and the stream-ordered
+    frames of the copy equal the original's bit for bit."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    n, W, H = 50_000, 960, 540
+    g = Y.gaussians_c2(n, seed=13)
+    g["means"][1::41] = g["means"][0::41][: len(g["means"][1::41])]
+    ubo = _gauss_ubo(W, H)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H)
+    r = Renderer(0, publish_splat_buffers=True)
+    try:
+        dg = {k: _dev(v) for k, v in g.items()}
+        sg = r.sort_gaussians_spatial(dg)
+        ids = sg["ids"].cpu().numpy()
+        assert sorted(ids.tolist()) == list(range(n)) and not np.array_equal(ids, np.arange(n))
+        np.testing.assert_array_equal(sg["means"].cpu().numpy(), g["means"][ids])
+        np.testing.assert_array_equal(sg["colors"].cpu().numpy(), g["colors"][ids])
+        for frame in range(2):  # three launches, then fused
+            out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            st = r.splat_gaussians(sg, ubo, W, H, out, want_stats=True)
+            torch.cuda.synchronize()
+            assert st.fused == frame
+            _check_published(r, st, ref, out, n, f"sorted copy, frame {frame}")
+        a = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        b = torch.zeros_like(a)
+        for _ in range(2):
+            r.splat_gaussians(dg, ubo, W, H, a)
+            r.splat_gaussians(sg, ubo, W, H, b)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        assert r.splat_status().frames == 0
+    finally:
+        r.close()
+
+
+def test_gaussians_fused_row_overflow(native_lib, oracle_lib):
+    """A fused frame whose densest tile outgrows the rows sized from the previous frame: without stats
+    it is skipped (output untouched) and reported, the next frame sizes its rows from it and renders
+    the oracle's frame; with stats the call re-runs it through the three launches (complete)."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H = 320, 180
+    ubo = _gauss_ubo(W, H)
+    sparse = {k: _dev(v) for k, v in Y.gaussians_c2(500, seed=2).items()}
+    g = Y.gaussians_c2(20_000, seed=5)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H)
+    assert int(np.diff(ref["ranges"].reshape(-1, 2), axis=1).max()) > 320  # above the 256-pair rows
+    dg = {k: _dev(v) for k, v in g.items()}
+    for with_stats in (False, True):
+        r = Renderer(0, publish_splat_buffers=True)
+        try:
+            r.splat_gaussians(sparse, ubo, W, H, torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"),
+                              want_stats=True)  # rows of 256 pairs from here
+            out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+            if with_stats:
+                st = r.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
+                assert st.fused == 0 and r.splat_status().frames == 0  # re-run through three launches
+                _check_published(r, st, ref, out, 20_000, "re-run")
+            else:
+                r.splat_gaussians(dg, ubo, W, H, out)
+                s1 = r.splat_status()
+                assert s1.frames == 1, s1.frames
+                assert bool((out == -7.0).all()), "a skipped frame must leave its output untouched"
+            out2 = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            st2 = r.splat_gaussians(dg, ubo, W, H, out2, want_stats=True)
+            assert st2.fused == 1 and r.splat_status().frames == 0
+            _check_published(r, st2, ref, out2, 20_000, "after the overflow")
+        finally:
+            r.close()
+
+
 def test_gaussians_tile_row_shards_compose(renderer, oracle_lib):
     """§8e screen-tile shard: rendering tile rows [0,a) and [a,gy) separately == the full frame, and
     the composed shards against the oracle's frame (1e-4 relative L2)."""

@@ -19,6 +19,15 @@ def main():
     n = int(os.environ.get("GS_N", "100000"))
     W, H = int(os.environ.get("GS_W", "1920")), int(os.environ.get("GS_H", "1080"))
     g = Y.gaussians_c2(n, seed=1)
+    if os.environ.get("GS_SORTED", "0") == "1":  # experiment: Gaussians in 3D Morton order of their means
+        m = g["means"]
+        q = ((m - m.min(0)) / np.maximum(m.max(0) - m.min(0), 1e-30) * 1023).astype(np.uint64)
+        code = np.zeros(len(m), np.uint64)
+        for b in range(10):
+            for a in range(3):
+                code |= ((q[:, a] >> np.uint64(b)) & np.uint64(1)) << np.uint64(3 * b + a)
+        order = np.argsort(code, kind="stable")
+        g = {k: np.ascontiguousarray(v[order]) for k, v in g.items()}
     dg = {k: torch.from_numpy(v).cuda() for k, v in g.items()}
     ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), cornell_box_scene(), 0)
     img = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
