@@ -673,9 +673,10 @@ def main():
 
     # ------------------------------------------------------------------ C5: the 8-GPU config
     # 1M-tri atrium + 10M C2-distributed Gaussians in its camera frame, 3840x2160, 256 spp in total.
-    # Rank g traces samples g, g+N, ... (256/N each, SUM), one all-reduce of the radiance (every rank
-    # needs the frame under its splat rows), primary-hit depth, splat-over of its tile rows into a
-    # zeroed frame, one reduce of the disjoint composites to rank 0 (strong scaling).
+    # Rank g traces samples g, g+N, ... (256/N each, SUM), a reduce-scatter of the radiance by the
+    # ranks' tile rows (each receives the sums under its own splat rows), mean + primary-hit depth,
+    # splat-over of its tile rows, row gather to rank 0 (dist.render_hybrid_frame; SURVEY 8e: strong
+    # scaling).
     if not args.no_c5 and not args.no_pt:
         from pathtracer_gaussiansplatting_amd import ACCUM_SUM as _SUM
         from pathtracer_gaussiansplatting_amd import dist as D
@@ -693,15 +694,21 @@ def main():
         dep5 = torch.zeros((H5, W5), dtype=torch.float32, device="cuda")
         comp5 = torch.zeros((H5, W5, 4), dtype=torch.float32, device="cuda")
         rows5 = D.tile_row_shard(rank, world, H5)
+        rows5_all = [D.tile_row_shard(k, world, H5) for k in range(world)]
 
         def c5_frame(want_stats=False):
+            if world == 1 or native_comm:
+                # dist.render_hybrid_frame: sample shard, reduce-scatter of the radiance by tile rows (each
+                # rank receives only its rows' sums), mean + depth, splat-over of its rows, row gather
+                u5 = make_ubo(pose5, sc5, 0, ambient=(0.3, 0.4, 0.5, 1.0), height=H5)
+                D.render_hybrid_frame(r, dg5, u5, W5, H5, acc5, dep5, comp5, SPP5, rank, world, tile_rows=rows5_all,
+                                      stream=stream, want_stats=want_stats)
+                return
+            # gloo rehearsal (ranks sharing one GPU: no CUDA reduce / send in gloo): full-frame all-reduces
             u5 = make_ubo(pose5, sc5, rank, ambient=(0.3, 0.4, 0.5, 1.0), height=H5)
             acc5.zero_()
             r.trace_camera(u5, W5, H5, acc5, spp=SPP5 // world, frame_stride=world, mode=_SUM, stream=stream)
-            if native_comm:
-                r.allreduce_radiance(acc5, stream=stream)  # RCCL through the library's communicator
-            else:
-                D.all_reduce_sum(acc5)
+            D.all_reduce_sum(acc5)
             mean5 = D.resolve_mean(acc5)
             r.trace_depth(u5, W5, H5, dep5, stream=stream)
             comp5.zero_()
@@ -728,6 +735,9 @@ def main():
                                  f"in total ({SPP5 // world} per GPU), sample shard + tile-row shard x{world}",
                      "ms_per_frame": round(d5 * 1e3, 2), "mrays_per_s": round(rays5 / d5 / 1e6, 1),
                      "gsplats_per_s": round(G5 / d5 / 1e9, 4), "scaling": "strong",
+                     "collectives": ("reduce-scatter of the radiance by tile rows + row gather (RCCL, "
+                                     "dist.render_hybrid_frame)") if (world == 1 or native_comm) else
+                                    "gloo rehearsal: full-frame all-reduces",
                      "bvh_nodes": int(info5.num_bvh_nodes), "bvh_depth": int(info5.bvh_depth)}
         del dg5, acc5, dep5, comp5
 

@@ -378,7 +378,7 @@ int ptgs_splat_gaussians_views(ptgs_ctx* ctx, const ptgs_gaussians* g, uint32_t 
 
 /* Front end. Once a finished frame of the context's workspace has reported its largest tile, frames
  * run a single-launch front end: per-tile key rows of a fixed capacity (a power of two >= 1.25x that
- * tile, <= 8192 pairs) filled through per-tile atomic reservations, instead of the exact tile
+ * tile, <= 2048 pairs) filled through per-tile atomic reservations, instead of the exact tile
  * segments of count + column scan + scatter (first frame, larger tiles, PTGS_GS_FRONTEND=three).
  * Both give the same keys, values, ranges and image. A frame with a tile above its row capacity is
  * skipped like an over-capacity frame (counted by ptgs_splat_status_read; with stats it is re-run
@@ -405,6 +405,10 @@ typedef struct ptgs_splat_status {
     uint32_t views[PTGS_MAX_VIEWS];
     uint32_t pair_capacity;
     uint32_t last_pairs;
+    uint32_t touched_runs;  /* slot 0's latest frame: (front-end workgroup, tile) runs, i.e. per-tile
+                             * reservations of the fused front end / nonzero histogram entries of the
+                             * count: the spatial coherence of the Gaussians' order */
+    uint32_t fused;         /* slot 0's latest frame ran the fused front end */
 } ptgs_splat_status;
 int ptgs_splat_status_read(ptgs_ctx* ctx, ptgs_splat_status* out, void* hip_stream);
 
@@ -508,6 +512,12 @@ int ptgs_allreduce_radiance(ptgs_ctx* ctx, float* accum, size_t n_floats, void* 
  * row_ranges holds every rank's range (2 x nranks, identical on all ranks). Stream-ordered. */
 int ptgs_gather_rows(ptgs_ctx* ctx, float* image, uint32_t width, uint32_t height, const uint32_t* row_ranges,
                      int root, void* hip_stream);
+/* Reduce-scatter by rows (the C5 hybrid's radiance): afterwards rank g's rows [row_ranges[2 g],
+ * row_ranges[2 g + 1]) of its RGBA32F image hold the SUM over all ranks of those rows (other rows
+ * unspecified); one ncclReduce per rank's rows (root = that rank) in one group: about one frame sent
+ * per rank instead of an all-reduce's two. row_ranges as ptgs_gather_rows. Stream-ordered. */
+int ptgs_reduce_scatter_rows(ptgs_ctx* ctx, float* image, uint32_t width, uint32_t height, const uint32_t* row_ranges,
+                             void* hip_stream);
 
 /* ---------------- output encode (blit rgba32f -> B8G8R8A8_SRGB, engine.cpp:2004-2020) --------- */
 /* rgba8 (device W*H u32, R in the low byte): linear -> sRGB8 of clamp(rgb,0,1), alpha 255. */

@@ -147,7 +147,7 @@ class SplatStats(C.Structure):
 class SplatStatus(C.Structure):
     """ptgs_splat_status: frames the stream-ordered splat skipped (pair buffer too small)."""
     _fields_ = [("frames", C.c_uint64), ("views", C.c_uint32 * 8), ("pair_capacity", C.c_uint32),
-                ("last_pairs", C.c_uint32)]
+                ("last_pairs", C.c_uint32), ("touched_runs", C.c_uint32), ("fused", C.c_uint32)]
 
 
 class SplatBuffers(C.Structure):
@@ -205,6 +205,7 @@ SYMBOLS = {
     "ptgs_reduce_radiance": (_I, [_P, _P, C.c_size_t, C.c_int, _P]),
     "ptgs_allreduce_radiance": (_I, [_P, _P, C.c_size_t, _P]),
     "ptgs_gather_rows": (_I, [_P, _P, C.c_uint32, C.c_uint32, _P, C.c_int, _P]),
+    "ptgs_reduce_scatter_rows": (_I, [_P, _P, C.c_uint32, C.c_uint32, _P, _P]),
     "ptgs_splat_stage_ms": (_I, [_P, _FP]),
     "ptgs_encode_srgb8": (_I, [_P, _P, _U, _U, _P, _P]),
     "ptgs_device_alloc": (_I, [_P, C.c_size_t, C.POINTER(_P)]),

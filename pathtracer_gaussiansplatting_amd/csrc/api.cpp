@@ -236,6 +236,20 @@ int ptgs_gather_rows(ptgs_ctx* c, float* image, uint32_t width, uint32_t height,
   return PTGS_OK;
 }
 
+int ptgs_reduce_scatter_rows(ptgs_ctx* c, float* image, uint32_t width, uint32_t height, const uint32_t* row_ranges,
+                             void* stream) {
+  if (!c || !image || !row_ranges) return PTGS_EINVAL;
+  if (!c->comm) return fail(c, PTGS_EINVAL, "no communicator (ptgs_comm_create)");
+  if (!is_device_ptr(image)) return fail(c, PTGS_EINVAL, "image is not a device pointer");
+  for (int g = 0; g < c->comm_ranks; ++g)
+    if (row_ranges[2 * g] > row_ranges[2 * g + 1] || row_ranges[2 * g + 1] > height)
+      return fail(c, PTGS_EINVAL, "bad row range of rank %d", g);
+  HIPCHK(c, hipSetDevice(c->device));
+  int e = comm_reduce_rows(c->comm, image, (size_t)width * 4u, row_ranges, c->comm_ranks, (hipStream_t)stream);
+  if (e) return fail(c, PTGS_EHIP, "ncclReduce: %s", comm_error(e));
+  return PTGS_OK;
+}
+
 const char* ptgs_last_error(const ptgs_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
@@ -720,6 +734,7 @@ int ptgs_splat_status_read(ptgs_ctx* c, ptgs_splat_status* out, void* stream) {
     out->pair_capacity = std::min(out->pair_capacity, cap);
     out->last_pairs = std::max(out->last_pairs, last);
   }
+  if (c->splat) splat_front_end_info(c->splat, &out->touched_runs, &out->fused);
   return PTGS_OK;
 }
 

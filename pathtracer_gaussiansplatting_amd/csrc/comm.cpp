@@ -136,4 +136,24 @@ int comm_gather_rows(void* comm, float* buf, size_t row_floats, const uint32_t* 
   return (int)(e != ncclSuccess ? e : e2);
 }
 
+// Reduce-scatter by rows: every rank g receives, in its own buffer's rows [range[2 g], range[2 g + 1]),
+// the SUM over the ranks of those rows (the other rows are left as they were): one ncclReduce per
+// rank's slice (root g, in place), all in one group so they proceed together. Each rank sends about
+// one frame ((G-1)/G of it) instead of an all-reduce's two; the C5 hybrid needs the path-traced
+// radiance only under the tile rows it composites.
+int comm_reduce_rows(void* comm, float* buf, size_t row_floats, const uint32_t* range, int nranks, hipStream_t s) {
+  Rccl& r = rccl();
+  if (!r.ok) return -1;
+  nccl_comm_t c = (nccl_comm_t)comm;
+  ncclResult_t e = r.group_start();
+  if (e != ncclSuccess) return (int)e;
+  for (int g = 0; g < nranks && e == ncclSuccess; ++g) {
+    if (range[2 * g + 1] <= range[2 * g]) continue;
+    float* p = buf + (size_t)range[2 * g] * row_floats;
+    e = r.reduce(p, p, (size_t)(range[2 * g + 1] - range[2 * g]) * row_floats, ncclFloat32, ncclSum, g, c, s);
+  }
+  ncclResult_t e2 = r.group_end();
+  return (int)(e != ncclSuccess ? e : e2);
+}
+
 }  // namespace ptgs

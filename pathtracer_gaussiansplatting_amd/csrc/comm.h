@@ -17,5 +17,6 @@ int comm_reduce_sum(void* comm, float* buf, size_t n, int root, hipStream_t s);
 int comm_allreduce_sum(void* comm, float* buf, size_t n, hipStream_t s);
 int comm_gather_rows(void* comm, float* buf, size_t row_floats, const uint32_t* range, int nranks, int rank, int root,
                      hipStream_t s);
+int comm_reduce_rows(void* comm, float* buf, size_t row_floats, const uint32_t* range, int nranks, hipStream_t s);
 
 }  // namespace ptgs

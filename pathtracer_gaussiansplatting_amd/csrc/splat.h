@@ -29,6 +29,8 @@ hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs);
 void splat_status(SplatWorkspace* w, bool clear, uint32_t* skipped, uint32_t* capacity, uint32_t* last_pairs);
 // the latest pair count any frame of this workspace published (a hint: no wait)
 uint32_t splat_pair_hint(const SplatWorkspace* w);
+// the latest frame's touched (workgroup, tile) runs and whether it ran the fused front end
+void splat_front_end_info(const SplatWorkspace* w, uint32_t* touched_runs, uint32_t* fused);
 void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out);
 hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long** keys);
 

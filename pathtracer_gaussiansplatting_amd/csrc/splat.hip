@@ -64,6 +64,7 @@ struct SplatWorkspace {
   bool hint_recorded = false;
   hipEvent_t hint_event = nullptr;
   bool last_fused = false;    // the last frame ran the fused front end
+  uint32_t fe_hold = 0;       // frames left on the three-launch front end (policy)
   uint32_t* k_host = nullptr;  // pinned, coherent [8]: K, largest tile, large tiles, skipped frames,
                                // fused reservations, fused overflow
   uint32_t* k_dev = nullptr;   // its device-side address
@@ -433,7 +434,17 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
   }
   __syncthreads();
   uint32_t* row = hist + (size_t)blockIdx.y * bg.tiles + ty0 * bg.grid_x;
-  for (uint32_t k = threadIdx.x; k < nt; k += GS_COUNT_THREADS) row[k] = s_hist[k];
+  uint32_t nz = 0;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_COUNT_THREADS) {
+    const uint32_t c = s_hist[k];
+    row[k] = c;
+    nz += c != 0u;
+  }
+  // touched (chunk, tile) entries, the front-end policy's measure of spatial coherence (the fused
+  // path would reserve each with an atomic): summed into total[2]; the scatter's block (0, 0) hands
+  // it to the host (k_host[4]) and re-arms it
+  for (int off = 32; off > 0; off >>= 1) nz += (uint32_t)__shfl_xor((int)nz, off);
+  if ((threadIdx.x & 63u) == 0 && nz) atomicAdd(total + 2, nz);
 }
 
 // One 256-work-item block per 64-tile group g: wave w sums chunks [w*cpw, (w+1)*cpw) of the group's
@@ -539,6 +550,10 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     total[0] = carry;
     __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);      // largest tile (the next sort's LDS size)
     __atomic_store_n(k_host + 2, large_ctr[0], __ATOMIC_RELAXED);  // large tiles (the next sort grid)
+    __atomic_store_n(k_host + 4, total[2], __ATOMIC_RELAXED);      // touched (chunk, tile) entries
+    __atomic_store_n(k_host + 5, 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(k_host + 6, 2u, __ATOMIC_RELAXED);  // published by: three launches
+    total[2] = 0;
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
     // a frame that does not fit is skipped by this kernel, the sort and the blend: count it for
     // ptgs_splat_status_read (one writer per workspace: its frames are ordered on one stream)
@@ -601,7 +616,8 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
 // The blend reads the tile's count from its cursor and zeroes it (cursors are zero between frames).
 // A tile whose count exceeds scap marks the frame (fz[2] = seq): sort and blend skip it, the host
 // counts it and falls back to the three-launch path. fz: [0] pairs, [1] largest tile above 256,
-// [2] overflow sequence, [3] reservations (atomics), published to the host by the blend.
+// [2] overflow sequence, [3] reservations (atomics), [4] tiles above GS_MID pairs; published to the
+// host by the blend.
 #ifndef GS_FUSED_THREADS
 #define GS_FUSED_THREADS 512
 #endif
@@ -671,7 +687,10 @@ __global__ __launch_bounds__(GS_FUSED_THREADS) void gs_bin_fused_kernel(SplatCam
       pairs += c;
       ++res;
       if (base + c > scap) __hip_atomic_store(fz + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (base + c > 256u) atomicMax(fz + 1, base + c);
+      if (base + c > 256u) {
+        atomicMax(fz + 1, base + c);
+        if (base <= GS_MID && base + c > GS_MID) atomicAdd(fz + 4, 1u);  // (one crossing per tile)
+      }
     }
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -1073,14 +1092,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
       const uint32_t big = fu.fz[1];
       __atomic_store_n(fu.k_host + 1, big > 256u ? big : 256u, __ATOMIC_RELAXED);  // largest tile (bound)
-      __atomic_store_n(fu.k_host + 2, 0u, __ATOMIC_RELAXED);
+      __atomic_store_n(fu.k_host + 2, fu.fz[4], __ATOMIC_RELAXED);                  // large tiles
       __atomic_store_n(fu.k_host + 4, fu.fz[3], __ATOMIC_RELAXED);                  // reservations
       __atomic_store_n(fu.k_host + 5, ovf ? 1u : 0u, __ATOMIC_RELAXED);            // tile above scap
+      __atomic_store_n(fu.k_host + 6, 1u, __ATOMIC_RELAXED);                       // published by: fused
       if (ovf) __atomic_store_n(fu.k_host + 3, __atomic_load_n(fu.k_host + 3, __ATOMIC_RELAXED) + 1u, __ATOMIC_RELAXED);
       __atomic_store_n(fu.k_host, fu.fz[0], __ATOMIC_RELAXED);
       fu.fz[0] = 0;
       fu.fz[1] = 0;
       fu.fz[3] = 0;
+      fu.fz[4] = 0;
       __threadfence_system();
     }
     if (ovf) {  // a tile did not fit its row: the frame is skipped (counted); cursors re-armed
@@ -1165,11 +1186,18 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     s_key[tid] = key;  // ~0 above n
     __syncthreads();
     uint32_t r = 0;
-    if (wave * 64u < n)
-      for (uint32_t j = 0; j < n; j += 2) {
-        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(s_key + j);
-        r += (uint32_t)(x.x < key) + (uint32_t)(x.y < key);
+    if (wave * 64u < n) {
+      // eight keys per step, four uniform reads in flight (entries n .. 255 hold ~0: never below a key)
+      const uint32_t nu = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
+      for (uint32_t j = 0; j < nu; j += 8) {
+        const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_key + j);
+        const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_key + j + 2);
+        const ulonglong2 x2 = *reinterpret_cast<const ulonglong2*>(s_key + j + 4);
+        const ulonglong2 x3 = *reinterpret_cast<const ulonglong2*>(s_key + j + 6);
+        r += ((uint32_t)(x0.x < key) + (uint32_t)(x0.y < key)) + ((uint32_t)(x1.x < key) + (uint32_t)(x1.y < key)) +
+             ((uint32_t)(x2.x < key) + (uint32_t)(x2.y < key)) + ((uint32_t)(x3.x < key) + (uint32_t)(x3.y < key));
       }
+    }
     __syncthreads();  // every read of the keys is done before records overwrite them
     if (tid < n) {
       s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
@@ -1230,10 +1258,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         s_key[tid + GS_BLOCK] = k1;
         __syncthreads();
         uint32_t r0 = 0, r1 = 0;
-        for (uint32_t j = 0; j < n; j += 2) {
+        const uint32_t nu = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
+        for (uint32_t j = 0; j < nu; j += 4) {  // (entries n .. 511 hold ~0)
           const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(s_key + j);
-          r0 += (x.x < k0) + (x.y < k0);
-          r1 += (x.x < k1) + (x.y < k1);
+          const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(s_key + j + 2);
+          r0 += ((x.x < k0) + (x.y < k0)) + ((y.x < k0) + (y.y < k0));
+          r1 += ((x.x < k1) + (x.y < k1)) + ((y.x < k1) + (y.y < k1));
         }
         __syncthreads();
         if (tid < n) s_key[r0] = k0;
@@ -1559,19 +1589,31 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   // has published its largest tile (the rows' capacity scap follows it with 1/4 headroom, a power of
   // two in [256, GS_FUSED_MAX_SCAP]); otherwise, or above that capacity, count + colscan + scatter.
 #ifndef GS_FUSED_MAX_SCAP
-#define GS_FUSED_MAX_SCAP 8192u
+#define GS_FUSED_MAX_SCAP 2048u  // larger tiles (1M Gaussians at 1080p): three launches measured faster
 #endif
 #ifndef GS_FRONTEND_DEFAULT
 #define GS_FRONTEND_DEFAULT 1  // 0: always three launches
 #endif
+#ifndef GS_FUSED_RUNS_PER_TILE
+#define GS_FUSED_RUNS_PER_TILE 16u
+#endif
+  // policy (PTGS_GS_FRONTEND unset): the fused path while its frames reserve at most
+  // GS_FUSED_RUNS_PER_TILE runs per tile (Gaussians in a spatially coherent order: each workgroup
+  // touches a compact set of tiles; in random order every workgroup touches most tiles and the
+  // reservations cost more than the histograms); otherwise three launches for 128 frames, then a probe
   static const int frontend = [] {
     const char* v = getenv("PTGS_GS_FRONTEND");  // "fused" / "three" (A/B switch)
     if (v && !strcmp(v, "three")) return 0;
     if (v && !strcmp(v, "fused")) return 1;
-    return GS_FRONTEND_DEFAULT;
+    return GS_FRONTEND_DEFAULT ? 2 : 0;
   }();
+  if (frontend == 2 && w->have_hint && w->k_host[6] == 1u && w->k_host[4] > GS_FUSED_RUNS_PER_TILE * tiles &&
+      w->fe_hold == 0)
+    w->fe_hold = 128;
+  const bool want_fused = frontend == 1 || (frontend == 2 && w->fe_hold == 0);
+  if (w->fe_hold) --w->fe_hold;
   uint32_t scap = 0;
-  if (frontend && w->have_hint && n) {
+  if (want_fused && w->have_hint && n) {
     const uint32_t big = std::max(256u, w->k_host[1] + w->k_host[1] / 4u);
     uint32_t c = 256;
     while (c < big && c < GS_FUSED_MAX_SCAP) c <<= 1;
@@ -1876,6 +1918,11 @@ void splat_status(SplatWorkspace* w, bool clear, uint32_t* skipped, uint32_t* ca
 }
 
 uint32_t splat_pair_hint(const SplatWorkspace* w) { return w->k_host ? w->k_host[0] : 0u; }
+
+void splat_front_end_info(const SplatWorkspace* w, uint32_t* touched_runs, uint32_t* fused) {
+  *touched_runs = w->k_host ? w->k_host[4] : 0u;
+  *fused = w->last_fused ? 1u : 0u;
+}
 
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms) {
   for (int k = 0; k < 6; ++k) out_ms[k] = 0.0f;

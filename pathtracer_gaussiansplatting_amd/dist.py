@@ -105,6 +105,26 @@ def gather_rows(image, pixel_ranges, dst: int = 0, renderer=None, group=None, st
     return image
 
 
+def reduce_scatter_rows(image, pixel_ranges, renderer=None, group=None, stream=None):
+    """Afterwards every rank's own pixel rows [r0, r1) of image ((H, W, 4) float32) hold the SUM over
+    the ranks of those rows (other rows unspecified): ptgs_reduce_scatter_rows through the library's
+    communicator (one ncclReduce per rank's rows, grouped), else one torch.distributed reduce per
+    rank's rows to that rank. About one frame per rank on the wire instead of an all-reduce's two."""
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return image
+    if len(pixel_ranges) != dist.get_world_size(group):
+        raise ValueError("reduce_scatter_rows needs one (r0, r1) per rank")
+    if renderer is not None and getattr(renderer, "comm_world", 0) > 1:
+        renderer.reduce_scatter_rows(image, pixel_ranges, stream=stream)
+        return image
+    with _on_stream(image, stream):
+        for g, (r0, r1) in enumerate(pixel_ranges):
+            if r1 > r0:
+                dist.reduce(image[r0:r1], dst=g, op=dist.ReduceOp.SUM, group=group)
+    return image
+
+
 class _on_stream:
     """torch.cuda.stream(stream) for device tensors (collectives issued after the stream's work);
     nothing for host tensors or stream=None."""
@@ -174,3 +194,39 @@ def render_gaussian_frame(renderer, gaussians: dict, ubo, width: int, height: in
     if rows[1] > rows[0]:
         renderer.splat_gaussians(gaussians, ubo, width, height, out, bg=bg, tile_rows=rows, stream=stream)
     return gather_rows(out, [pixel_rows(r, height) for r in tile_rows], dst=0, renderer=renderer, stream=stream)
+
+
+def render_hybrid_frame(renderer, gaussians: dict, ubo, width: int, height: int, accum, depth, out, spp_total: int,
+                        rank: int, world: int, frame0: int = 0, tile_rows=None, stream=None, **splat_kw):
+    """The C5 hybrid frame ("both, with the depth composite done after the reduce"), sharded
+    so that each rank moves only what its rows need:
+      1. rank g traces samples g, g + G, ... (spp_total / G of them, SUM) of the whole frame into accum;
+      2. reduce-scatter of accum by the ranks' tile rows (reduce_scatter_rows): rank g ends up with the
+         full radiance sum of its own rows only;
+      3. their running mean (rgb / count, a = 1) into out's rows, the primary-hit depth;
+      4. the 3DGS splat-over composite of its tile rows (ptgs_splat_gaussians_over, out as "under");
+      5. the row gather to rank 0 (gather_rows): out is the composed frame there.
+    accum: (H, W, 4) sum buffer; depth: (H, W); out: (H, W, 4). tile_rows: every rank's (begin, end)
+    tile rows (default tile_row_shard). Equals the single-process frame (trace spp_total, mean, depth,
+    splat over) up to the float order of the radiance sums (~1e-7 relative)."""
+    from ._abi import ACCUM_SUM
+    if spp_total % world:
+        raise ValueError(f"spp_total {spp_total} is not a multiple of the world size {world}")
+    if tile_rows is None:
+        tile_rows = [tile_row_shard(g, world, height) for g in range(world)]
+    px = [pixel_rows(r, height) for r in tile_rows]
+    f, stride = sample_shard(rank, world, frame0)
+    ubo.frame_count = f
+    with _on_stream(accum, stream):
+        accum.zero_()
+    renderer.trace_camera(ubo, width, height, accum, spp=spp_total // world, frame_stride=stride, mode=ACCUM_SUM,
+                          stream=stream)
+    reduce_scatter_rows(accum, px, renderer=renderer, stream=stream)
+    renderer.trace_depth(ubo, width, height, depth, stream=stream)
+    p0, p1 = px[rank]
+    if p1 > p0:
+        with _on_stream(out, stream):
+            out[p0:p1] = resolve_mean(accum[p0:p1])
+        renderer.splat_gaussians(gaussians, ubo, width, height, out, tile_rows=tile_rows[rank], over=(depth, out),
+                                 stream=stream, **splat_kw)
+    return gather_rows(out, px, dst=0, renderer=renderer, stream=stream)

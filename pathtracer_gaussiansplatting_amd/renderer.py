@@ -183,6 +183,19 @@ class Renderer:
         rc = self.lib.ptgs_gather_rows(self._h, _ptr(image), W, H, rr.ctypes.data, root, _stream(stream))
         self._chk(rc, "ptgs_gather_rows")
 
+    def reduce_scatter_rows(self, image, row_ranges, stream=None):
+        """ptgs_reduce_scatter_rows: afterwards this rank's pixel rows of the (H, W, 4) float32 image hold
+        the SUM over the ranks of those rows; row_ranges: one (r0, r1) per rank, identical everywhere."""
+        H, W = int(image.shape[0]), int(image.shape[1])
+        world = getattr(self, "comm_world", 0)
+        if len(row_ranges) != world:
+            raise ValueError(f"reduce_scatter_rows needs one (r0, r1) per rank: {len(row_ranges)} given, world {world}")
+        rr = np.asarray(row_ranges, np.uint32).reshape(-1)
+        if rr.size != 2 * world:
+            raise ValueError("reduce_scatter_rows: every row range is a (r0, r1) pair")
+        rc = self.lib.ptgs_reduce_scatter_rows(self._h, _ptr(image), W, H, rr.ctypes.data, _stream(stream))
+        self._chk(rc, "ptgs_reduce_scatter_rows")
+
     def set_flags(self, flags: int):
         self._flags = flags
         self._chk(self.lib.ptgs_set_flags(self._h, flags | self._publish), "ptgs_set_flags")
