@@ -58,15 +58,18 @@ struct SplatWorkspace {
   DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, tile_info,
       group_total, tile_slots, point_keys, total, rect, large, large_ctr, sort_scratch;
   DevBuf cursor, fz, pub_offs, keys_pub, vals_pub;  // fused front end (see gs_bin_fused_kernel)
-  DevBuf dbg_depths;
+  DevBuf dbg_depths, fzp, nzbuf;
   uint32_t seq = 0;           // fused frames enqueued (the overflow word's tag)
   bool have_hint = false;     // a finished frame has published its largest tile: the fused path can size its rows
   bool hint_recorded = false;
   hipEvent_t hint_event = nullptr;
   bool last_fused = false;    // the last frame ran the fused front end
-  uint32_t fe_hold = 0;       // frames left on the three-launch front end (policy)
-  uint32_t* k_host = nullptr;  // pinned, coherent [8]: K, largest tile, large tiles, skipped frames,
-                               // fused reservations, fused overflow
+  // front-end policy: 0 fused, 1 probing (one fused frame, seq fe_probe, until its result is in),
+  // 2 three launches for fe_hold more frames
+  uint32_t fe_state = 1, fe_probe = 0, fe_hold = 0;
+  uint32_t* k_host = nullptr;  // pinned, coherent [16]: K, largest tile, large tiles, skipped frames,
+                               // touched runs, fused overflow, publishing path (1 fused / 2 three),
+                               // latest fused frame's seq, its runs
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
@@ -85,7 +88,7 @@ void splat_workspace_destroy(SplatWorkspace* w) {
   DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rec, &w->radii, &w->touched, &w->pairs, &w->keys_out,
                    &w->vals_out, &w->ranges, &w->hist, &w->tile_info, &w->group_total, &w->tile_slots, &w->point_keys,
                    &w->total, &w->rect, &w->large, &w->large_ctr, &w->sort_scratch, &w->cursor, &w->fz,
-                   &w->pub_offs, &w->keys_pub, &w->vals_pub, &w->dbg_depths};
+                   &w->pub_offs, &w->keys_pub, &w->vals_pub, &w->dbg_depths, &w->fzp, &w->nzbuf};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
                                                                       uint32_t* __restrict__ hist,
                                                                       uint32_t* __restrict__ total,
                                                                       uint32_t* __restrict__ large_ctr,
-                                                                      uint32_t* k_host) {
+                                                                      uint32_t* k_host, uint32_t* __restrict__ nzbuf) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
   uint32_t ty0, ty1;
   gs_band(bg, ty0, ty1);
@@ -441,10 +444,17 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
     nz += c != 0u;
   }
   // touched (chunk, tile) entries, the front-end policy's measure of spatial coherence (the fused
-  // path would reserve each with an atomic): summed into total[2]; the scatter's block (0, 0) hands
-  // it to the host (k_host[4]) and re-arms it
+  // path would reserve each with an atomic), per workgroup; the scatter's block (0, 0) sums them for
+  // the host (k_host[4])
   for (int off = 32; off > 0; off >>= 1) nz += (uint32_t)__shfl_xor((int)nz, off);
-  if ((threadIdx.x & 63u) == 0 && nz) atomicAdd(total + 2, nz);
+  __shared__ uint32_t s_nz[GS_COUNT_THREADS / 64];
+  if ((threadIdx.x & 63u) == 0) s_nz[threadIdx.x >> 6] = nz;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < GS_COUNT_THREADS / 64; ++w) t += s_nz[w];
+    nzbuf[blockIdx.y * gridDim.x + blockIdx.x] = t;  // (summed by the scatter's block (0, 0): no fan-in atomics)
+  }
 }
 
 // One 256-work-item block per 64-tile group g: wave w sums chunks [w*cpw, (w+1)*cpw) of the group's
@@ -516,7 +526,8 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     BinGrid bg, const ushort4* __restrict__ rects, const float* __restrict__ depths, const uint32_t* __restrict__ ids,
     uint32_t n,
     const uint32_t* __restrict__ hist, const uint2* __restrict__ tile_info, const uint32_t* __restrict__ group_total,
-    uint32_t* __restrict__ total, const uint32_t* __restrict__ large_ctr, uint32_t* k_host, uint32_t cap,
+    uint32_t* __restrict__ total, const uint32_t* __restrict__ large_ctr, uint32_t* k_host,
+    const uint32_t* __restrict__ nzbuf, uint32_t nzn, uint32_t cap,
     uint2* __restrict__ ranges,
     unsigned long long* __restrict__ pairs, unsigned long long* __restrict__ tile_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];  // 2 * band_rows * grid_x + groups
@@ -546,14 +557,22 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     carry = all;
     __syncthreads();
   }
+  uint32_t nzsum = 0;
+  if (blockIdx.x == 0 && blockIdx.y == 0) {  // the count's touched entries (per workgroup)
+    for (uint32_t k = tid; k < nzn; k += GS_BIN_THREADS) nzsum += nzbuf[k];
+    for (int off = 32; off > 0; off >>= 1) nzsum += (uint32_t)__shfl_xor((int)nzsum, off);
+    if (lane == 0) s_part[wv] = nzsum;
+    __syncthreads();
+    nzsum = 0;
+    for (uint32_t w = 0; w < GS_BIN_THREADS / 64; ++w) nzsum += s_part[w];
+  }
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
     total[0] = carry;
     __atomic_store_n(k_host + 1, total[1], __ATOMIC_RELAXED);      // largest tile (the next sort's LDS size)
     __atomic_store_n(k_host + 2, large_ctr[0], __ATOMIC_RELAXED);  // large tiles (the next sort grid)
-    __atomic_store_n(k_host + 4, total[2], __ATOMIC_RELAXED);      // touched (chunk, tile) entries
+    __atomic_store_n(k_host + 4, nzsum, __ATOMIC_RELAXED);         // touched (chunk, tile) entries
     __atomic_store_n(k_host + 5, 0u, __ATOMIC_RELAXED);
     __atomic_store_n(k_host + 6, 2u, __ATOMIC_RELAXED);  // published by: three launches
-    total[2] = 0;
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
     // a frame that does not fit is skipped by this kernel, the sort and the blend: count it for
     // ptgs_splat_status_read (one writer per workspace: its frames are ordered on one stream)
@@ -615,9 +634,9 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
 // fixed by the per-tile sort (keys are unique), so keys / values / image equal the three-launch path.
 // The blend reads the tile's count from its cursor and zeroes it (cursors are zero between frames).
 // A tile whose count exceeds scap marks the frame (fz[2] = seq): sort and blend skip it, the host
-// counts it and falls back to the three-launch path. fz: [0] pairs, [1] largest tile above 256,
-// [2] overflow sequence, [3] reservations (atomics), [4] tiles above GS_MID pairs; published to the
-// host by the blend.
+// counts it and falls back to the three-launch path. fz: [1] largest tile above 256, [2] overflow
+// sequence, [4] tiles above GS_MID pairs; per workgroup fzp: (pairs, reservations); published to the
+// host by the blend's block (0, 0).
 #ifndef GS_FUSED_THREADS
 #define GS_FUSED_THREADS 512
 #endif
@@ -627,6 +646,8 @@ struct GsFused {  // the sort's and the blend's view of a fused-front-end frame 
   uint32_t* fz;       // counters (see above)
   uint32_t* k_host;   // pinned host words (published by blend block (0, 0))
   uint2* ranges;      // the tile ranges the blend writes (t * scap, t * scap + n)
+  uint32_t* fzp;      // per front-end workgroup: (pairs, reservations)
+  uint32_t nwg;
 };
 // GS_STAMP builds (tools/gs_stamps.py): per-workgroup s_memrealtime (100 MHz) stamps at phase
 // boundaries of the fused front end and the blend, read back with ptgs_debug_stamps.
@@ -649,6 +670,7 @@ __global__ __launch_bounds__(GS_FUSED_THREADS) void gs_bin_fused_kernel(SplatCam
                                                                          uint32_t scap, uint32_t seq,
                                                                          uint32_t* __restrict__ cursor,
                                                                          uint32_t* __restrict__ fz,
+                                                                         uint32_t* __restrict__ fzp,
                                                                          unsigned long long* __restrict__ tile_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
   __shared__ uint32_t s_red[2][GS_FUSED_THREADS / 64];
@@ -702,14 +724,15 @@ __global__ __launch_bounds__(GS_FUSED_THREADS) void gs_bin_fused_kernel(SplatCam
     s_red[1][wave] = res;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // per-workgroup partials (the blend's block (0, 0) sums them: no fan-in atomics)
     uint32_t p = 0, r = 0;
     for (uint32_t w = 0; w < GS_FUSED_THREADS / 64; ++w) {
       p += s_red[0][w];
       r += s_red[1][w];
     }
-    if (p) atomicAdd(fz, p);
-    if (r) atomicAdd(fz + 3, r);
+    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
+    fzp[2 * wg] = p;
+    fzp[2 * wg + 1] = r;
   }
   STAMP(0, 4);
 #ifdef GS_STAMP
@@ -1089,18 +1112,38 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     // fused front end: block (0, 0) hands the frame's counters to the host and re-arms them (the
     // fused kernel that produced them has finished; no other blend block reads them)
     const bool ovf = __hip_atomic_load(fu.fz + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fu.seq;
+    uint32_t fp = 0, fr = 0;  // the front end's pairs and reservations (block (0, 0) sums the partials)
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      for (uint32_t k = tid; k < fu.nwg; k += GS_BLOCK) {
+        fp += fu.fzp[2 * k];
+        fr += fu.fzp[2 * k + 1];
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        fp += (uint32_t)__shfl_xor((int)fp, off);
+        fr += (uint32_t)__shfl_xor((int)fr, off);
+      }
+      uint32_t* s_r = reinterpret_cast<uint32_t*>(s_arena);  // (before any other use of the arena)
+      if (lane == 0) {
+        s_r[wave] = fp;
+        s_r[4 + wave] = fr;
+      }
+      __syncthreads();
+      fp = (s_r[0] + s_r[1]) + (s_r[2] + s_r[3]);
+      fr = (s_r[4] + s_r[5]) + (s_r[6] + s_r[7]);
+      __syncthreads();
+    }
     if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
       const uint32_t big = fu.fz[1];
       __atomic_store_n(fu.k_host + 1, big > 256u ? big : 256u, __ATOMIC_RELAXED);  // largest tile (bound)
       __atomic_store_n(fu.k_host + 2, fu.fz[4], __ATOMIC_RELAXED);                  // large tiles
-      __atomic_store_n(fu.k_host + 4, fu.fz[3], __ATOMIC_RELAXED);                  // reservations
+      __atomic_store_n(fu.k_host + 4, fr, __ATOMIC_RELAXED);                        // reservations
+      __atomic_store_n(fu.k_host + 8, fr, __ATOMIC_RELAXED);                        // (the policy's copy)
       __atomic_store_n(fu.k_host + 5, ovf ? 1u : 0u, __ATOMIC_RELAXED);            // tile above scap
       __atomic_store_n(fu.k_host + 6, 1u, __ATOMIC_RELAXED);                       // published by: fused
+      __atomic_store_n(fu.k_host + 7, fu.seq, __ATOMIC_RELAXED);                   // ... this frame
       if (ovf) __atomic_store_n(fu.k_host + 3, __atomic_load_n(fu.k_host + 3, __ATOMIC_RELAXED) + 1u, __ATOMIC_RELAXED);
-      __atomic_store_n(fu.k_host, fu.fz[0], __ATOMIC_RELAXED);
-      fu.fz[0] = 0;
+      __atomic_store_n(fu.k_host, fp, __ATOMIC_RELAXED);
       fu.fz[1] = 0;
-      fu.fz[3] = 0;
       fu.fz[4] = 0;
       __threadfence_system();
     }
@@ -1514,6 +1557,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   bgrid.chunk = std::max(1u, (n + bgrid.chunks - 1) / bgrid.chunks);
   const size_t band_lds = (size_t)bgrid.band_rows * cam.grid_x * 4;
   if ((e = ensure(w->hist, (size_t)bgrid.chunks * tiles * 4))) return e;
+  if ((e = ensure(w->nzbuf, (size_t)bgrid.chunks * bgrid.bands * 4))) return e;
   if ((e = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e;
   if ((e = ensure(w->tile_info, (size_t)tiles * 8))) return e;
   if ((e = ensure(w->group_total, (size_t)bgrid.groups * 4))) return e;
@@ -1527,8 +1571,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = hipMemset(w->total.p, 0, 16))) return e;
   }
   if (!w->k_host) {
-    if ((e = hipHostMalloc((void**)&w->k_host, 32, hipHostMallocCoherent | hipHostMallocMapped))) return e;
-    std::memset(w->k_host, 0, 32);
+    if ((e = hipHostMalloc((void**)&w->k_host, 64, hipHostMallocCoherent | hipHostMallocMapped))) return e;
+    std::memset(w->k_host, 0, 64);
     if ((e = hipHostGetDevicePointer((void**)&w->k_dev, w->k_host, 0))) return e;
   }
 #ifndef GS_K_EVENT_FLAGS
@@ -1607,11 +1651,28 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if (v && !strcmp(v, "fused")) return 1;
     return GS_FRONTEND_DEFAULT ? 2 : 0;
   }();
-  if (frontend == 2 && w->have_hint && w->k_host[6] == 1u && w->k_host[4] > GS_FUSED_RUNS_PER_TILE * tiles &&
-      w->fe_hold == 0)
-    w->fe_hold = 128;
-  const bool want_fused = frontend == 1 || (frontend == 2 && w->fe_hold == 0);
-  if (w->fe_hold) --w->fe_hold;
+  // (a fused frame's runs reach the host asynchronously (k_host[4], tagged with its seq in k_host[7]):
+  // after a probe, frames use three launches until its result is in; a passing probe keeps the fused
+  // path, and each later fused result is checked again)
+  bool want_fused = frontend == 1;
+  if (frontend == 2) {
+    // k_host[7] / [8]: seq and runs of the latest fused frame (a three-launch frame does not touch them)
+    const bool result_in = w->k_host[7] == w->fe_probe;
+    const bool coherent = w->k_host[8] <= GS_FUSED_RUNS_PER_TILE * tiles;
+    if (w->fe_state == 0) {  // fused: re-checked on every fused result
+      if (w->k_host[7] && !coherent) {
+        w->fe_state = 2;
+        w->fe_hold = 128;
+      }
+    } else if (w->fe_state == 1 && w->fe_probe && result_in) {  // probing: the probe's result is in
+      w->fe_state = coherent ? 0 : 2;
+      w->fe_hold = coherent ? 0 : 128;
+    } else if (w->fe_state == 2 && --w->fe_hold == 0) {  // held: probe again
+      w->fe_state = 1;
+      w->fe_probe = 0;
+    }
+    want_fused = w->fe_state == 0 || (w->fe_state == 1 && w->fe_probe == 0);
+  }
   uint32_t scap = 0;
   if (want_fused && w->have_hint && n) {
     const uint32_t big = std::max(256u, w->k_host[1] + w->k_host[1] / 4u);
@@ -1637,7 +1698,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if (!e2) w->sort_attr = true;
     return e2;
   };
-  const GsFused no_fu = {0u, 0u, nullptr, nullptr, nullptr, nullptr};
+  const GsFused no_fu = {0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u};
 
   auto enqueue_fused = [&]() -> hipError_t {
     hipError_t e2;
@@ -1652,8 +1713,12 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
       if ((e2 = ensure(w->fz, 64))) return e2;
       if ((e2 = hipMemsetAsync(w->fz.p, 0, 64, s))) return e2;
     }
+    const uint32_t nwg = bgrid.bands * ((n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS);
+    if ((e2 = ensure(w->fzp, (size_t)nwg * 8))) return e2;
     const uint32_t seq = ++w->seq;
-    GsFused fu = {scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p};
+    if (w->fe_state == 1 && w->fe_probe == 0) w->fe_probe = seq;
+    GsFused fu = {scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
+                  (uint32_t*)w->fzp.p, nwg};
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers
     fpa.rects = nullptr;
     fpa.depths = nullptr;
@@ -1661,7 +1726,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
     fg.chunk = GS_FUSED_THREADS;
     hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks), dim3(GS_FUSED_THREADS), band_lds, s, cam, fpa, fg,
-                       scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (unsigned long long*)w->tile_slots.p);
+                       scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
+                       (unsigned long long*)w->tile_slots.p);
     if ((e2 = hipGetLastError())) return e2;
     if ((e2 = mark(1)) || (e2 = mark(2)) || (e2 = mark(3))) return e2;
     unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
@@ -1701,7 +1767,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     hipLaunchKernelGGL(gs_bin_scatter_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_BIN_THREADS),
                        2 * band_lds + (size_t)bgrid.groups * 4, s, bgrid, (const ushort4*)w->rect.p,
                        (const float*)w->depths.p, g->ids, n, (const uint32_t*)w->hist.p, (const uint2*)w->tile_info.p,
-                       (const uint32_t*)w->group_total.p, (uint32_t*)w->total.p, (const uint32_t*)w->large_ctr.p, w->k_dev, cap,
+                       (const uint32_t*)w->group_total.p, (uint32_t*)w->total.p, (const uint32_t*)w->large_ctr.p, w->k_dev,
+                       (const uint32_t*)w->nzbuf.p, bgrid.bands * bgrid.chunks, cap,
                        (uint2*)w->ranges.p, (unsigned long long*)w->pairs.p, (unsigned long long*)w->tile_slots.p);
     hipError_t e2 = hipGetLastError();
     if (e2) return e2;
@@ -1737,7 +1804,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e2 = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e2;
     // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
     hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_COUNT_THREADS), band_lds, s, cam, pa,
-                       bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev);
+                       bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev,
+                       (uint32_t*)w->nzbuf.p);
     if ((e2 = hipGetLastError())) return e2;
     if ((e2 = mark(1))) return e2;
     hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(GS_COLSCAN_THREADS), 0, s, bgrid, (uint32_t*)w->hist.p,

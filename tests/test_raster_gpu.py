@@ -340,8 +340,9 @@ def _check_published(r, st, ref, out, n, what):
                                    (3000, 3840, 2160)])    # 4K: four bands of tile rows
 def test_gaussians_fused_front_end(native_lib, oracle_lib, n, W, H):
     """The single-launch front end (per-tile rows filled through atomic reservations) runs from the
-    second frame of a context on: its sorted keys / values / ranges, radii / tiles touched (bit-exact)
-    and image (< 1e-4) equal the oracle's, as the first (three-launch) frame's do."""
+    second frame of a context on (Gaussians in Morton order: the policy keeps it): its sorted keys /
+    values / ranges, radii / tiles touched (bit-exact) and image (< 1e-4) equal the oracle's, as the
+    first (three-launch) frame's do."""
     from pathtracer_gaussiansplatting_amd import Renderer
     g = Y.gaussians_c2(n, seed=9)
     g["means"][1::53] = g["means"][0::53][: len(g["means"][1::53])]  # duplicated means: equal depths
@@ -349,13 +350,40 @@ def test_gaussians_fused_front_end(native_lib, oracle_lib, n, W, H):
     ref = oracle_lib.splat_gaussians(g, ubo, W, H, bg=(0.1, 0.2, 0.3))
     r = Renderer(0, publish_splat_buffers=True)
     try:
-        dg = {k: _dev(v) for k, v in g.items()}
+        dg = r.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
         for frame in range(3):
             out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
             st = r.splat_gaussians(dg, ubo, W, H, out, bg=(0.1, 0.2, 0.3), want_stats=True)
             torch.cuda.synchronize()
             assert st.fused == (frame > 0), (frame, st.fused)
             _check_published(r, st, ref, out, n, f"frame {frame}")
+    finally:
+        r.close()
+
+
+def test_gaussians_front_end_policy(native_lib, oracle_lib):
+    """Gaussians in their generated (random) order touch most tiles from every front-end workgroup:
+    the fused probe frame reports > 16 runs per tile and the next frames go back to three launches;
+    every frame is the oracle's."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    n, W, H = 100_000, 1920, 1080
+    g = Y.gaussians_c2(n, seed=9)
+    ubo = _gauss_ubo(W, H)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H)
+    r = Renderer(0, publish_splat_buffers=True)
+    try:
+        dg = {k: _dev(v) for k, v in g.items()}
+        got = []
+        for frame in range(4):
+            out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            st = r.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
+            torch.cuda.synchronize()
+            got.append(st.fused)
+            if frame == 1:
+                s = r.splat_status()
+                assert s.fused == 1 and s.touched_runs > 16 * st.tiles_x * st.tiles_y, s.touched_runs
+            _check_published(r, st, ref, out, n, f"frame {frame}")
+        assert got == [0, 1, 0, 0], got
     finally:
         r.close()
 
@@ -408,10 +436,10 @@ def test_gaussians_fused_row_overflow(native_lib, oracle_lib):
     g = Y.gaussians_c2(20_000, seed=5)
     ref = oracle_lib.splat_gaussians(g, ubo, W, H)
     assert int(np.diff(ref["ranges"].reshape(-1, 2), axis=1).max()) > 320  # above the 256-pair rows
-    dg = {k: _dev(v) for k, v in g.items()}
     for with_stats in (False, True):
         r = Renderer(0, publish_splat_buffers=True)
         try:
+            dg = r.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})  # (the policy keeps fused)
             r.splat_gaussians(sparse, ubo, W, H, torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"),
                               want_stats=True)  # rows of 256 pairs from here
             out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
