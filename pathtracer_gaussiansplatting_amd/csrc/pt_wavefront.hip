@@ -122,6 +122,12 @@ __device__ __forceinline__ void ss_fill(SlotStream& s, const uint8_t* __restrict
 #ifndef PTGS_WF_AH_CALL
 #define PTGS_WF_AH_CALL true  // textured any-hit out of line (pt_device.h anyhit_accept_call)
 #endif
+#ifndef PTGS_WF_AH_CALL_EXT
+#define PTGS_WF_AH_CALL_EXT PTGS_WF_AH_CALL
+#endif
+#ifndef PTGS_WF_AH_CALL_SHADOW
+#define PTGS_WF_AH_CALL_SHADOW PTGS_WF_AH_CALL
+#endif
 #ifndef PTGS_WF_LDS_EXT
 #define PTGS_WF_LDS_EXT PTGS_STACK  // extend kernel: LDS entries (39: 4 waves / SIMD, 86 VGPRs)
 #endif
@@ -261,11 +267,11 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_exte
       if (__all(leaf != WF_DONE || node == WF_DONE)) break;
     }
     if (leaf != WF_DONE) {
-      leaf_closest<STATS, TEX, PTGS_WF_AH_CALL>(sc, r, leaf, h, seed, tc);
+      leaf_closest<STATS, TEX, PTGS_WF_AH_CALL_EXT>(sc, r, leaf, h, seed, tc);
       leaf = WF_DONE;
     }
     if (node < 0) {
-      leaf_closest<STATS, TEX, PTGS_WF_AH_CALL>(sc, r, node, h, seed, tc);
+      leaf_closest<STATS, TEX, PTGS_WF_AH_CALL_EXT>(sc, r, node, h, seed, tc);
       node = pop();
     }
     if (node == WF_DONE) {
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_shad
         if (!tri_isect(r, mk3(ta.x, ta.y, ta.z), mk3(tb.x, tb.y, tb.z), mk3(tcv.x, tcv.y, tcv.z), t, u, v)) continue;
         if (!(t >= r.tmin && t <= r.tmax)) continue;
         if (sc.has_transparent && (sc.tri_flags[start + k] & 1u)) {
-          const bool acc = (TEX && PTGS_WF_AH_CALL) ? anyhit_accept_call(sc, f2u(ta.w), f2u(tb.w), u, v, seed, f2u(tcv.w))
+          const bool acc = (TEX && PTGS_WF_AH_CALL_SHADOW) ? anyhit_accept_call(sc, f2u(ta.w), f2u(tb.w), u, v, seed, f2u(tcv.w))
                                : anyhit_accept<TEX>(sc, f2u(ta.w), f2u(tb.w), u, v, seed, f2u(tcv.w));
           if (!acc) continue;
         }

@@ -666,21 +666,60 @@ __device__ unsigned long long g_gs_stamps[2][GS_STAMP_WG * GS_STAMP_N];
 #define STAMP(kind, k) do { } while (0)
 #define STAMP_SYNC() do { } while (0)
 #endif
-__global__ __launch_bounds__(GS_FUSED_THREADS) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
+#ifndef GS_FUSED_WG
+#define GS_FUSED_WG 1024  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
+#endif
+
+// Workgroup-cooperative pair walk of the fused front end: the chunk's rects (s_e: x0 | w << 16,
+// y0 | h << 16, key index, depth bits) and the inclusive scan of their areas (s_incl) are in LDS;
+// work-item t takes the contiguous pairs [t q, t q + q) of the chunk's P (q = ceil(P / GS_FUSED_WG)):
+// one binary search for its first pair, then it steps through the rects (a heavy Gaussian's pairs are
+// spread over the whole workgroup instead of one wave). f(key index, x, y, depth bits).
+template <typename F>
+__device__ __forceinline__ void gs_wg_walk(const uint32_t* s_incl, const uint4* s_e, uint32_t ng, uint32_t P, F f) {
+  const uint32_t q = (P + GS_FUSED_WG - 1) / GS_FUSED_WG;
+  uint32_t p = threadIdx.x * q;
+  const uint32_t p1 = min(P, p + q);
+  if (p >= p1) return;
+  uint32_t lo = 0, hi = ng - 1;  // first j with incl[j] > p
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s_incl[mid] > p) hi = mid;
+    else lo = mid + 1;
+  }
+  uint32_t j = lo;
+  uint4 e = s_e[j];
+  uint32_t w = e.x >> 16, r = p - (s_incl[j] - w * (e.y >> 16));
+  uint32_t ry = r / w, rx = r - ry * w;
+  for (;;) {
+    f(e.z, (e.x & 0xFFFFu) + rx, (e.y & 0xFFFFu) + ry, e.w);
+    if (++p >= p1) break;
+    if (++rx == w) {
+      rx = 0;
+      if (++ry == (e.y >> 16)) {  // next rect with pairs
+        do {
+          e = s_e[++j];
+        } while ((e.y >> 16) == 0u || (e.x >> 16) == 0u);
+        w = e.x >> 16;
+        ry = 0;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                          uint32_t scap, uint32_t seq,
                                                                          uint32_t* __restrict__ cursor,
                                                                          uint32_t* __restrict__ fz,
                                                                          uint32_t* __restrict__ fzp,
                                                                          unsigned long long* __restrict__ tile_slots) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
-  __shared__ uint32_t s_red[2][GS_FUSED_THREADS / 64];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // <= band_rows * grid_x
+  __shared__ uint32_t s_red[4][GS_FUSED_WG / 64];
+  __shared__ uint32_t s_incl[GS_FUSED_THREADS];
+  __shared__ uint4 s_e[GS_FUSED_THREADS];
   STAMP(0, 0);
   uint32_t ty0, ty1;
   gs_band(bg, ty0, ty1);
-  const uint32_t nt = (ty1 - ty0) * bg.grid_x, t0 = ty0 * bg.grid_x;
-  for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_THREADS) s_hist[k] = 0;
-  __syncthreads();
-  STAMP(0, 1);
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t i = blockIdx.y * bg.chunk + threadIdx.x;  // chunk <= GS_FUSED_THREADS (host)
   const bool own = threadIdx.x < bg.chunk && i < A.n;
@@ -690,28 +729,86 @@ __global__ __launch_bounds__(GS_FUSED_THREADS) void gs_bin_fused_kernel(SplatCam
   if (own) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
   uint32_t xw, yh;
   gs_clip(rc, ty0, ty1, xw, yh);
+  // the chunk's bounding tile rect (within the band): the LDS histogram covers only it, so zeroing
+  // and the reservation scan touch ~100 entries for a spatially coherent chunk instead of the band's
+  uint32_t bx0 = 0xFFFFu, by0 = 0xFFFFu, bx1 = 0u, by1 = 0u;
+  if (yh) {
+    bx0 = xw & 0xFFFFu;
+    bx1 = bx0 + (xw >> 16);
+    by0 = yh & 0xFFFFu;
+    by1 = by0 + (yh >> 16);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    bx0 = min(bx0, (uint32_t)__shfl_xor((int)bx0, off));
+    by0 = min(by0, (uint32_t)__shfl_xor((int)by0, off));
+    bx1 = max(bx1, (uint32_t)__shfl_xor((int)bx1, off));
+    by1 = max(by1, (uint32_t)__shfl_xor((int)by1, off));
+  }
+  if (lane == 0) {
+    s_red[0][wave] = bx0;
+    s_red[1][wave] = by0;
+    s_red[2][wave] = bx1;
+    s_red[3][wave] = by1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t w = 0; w < GS_FUSED_WG / 64; ++w) {
+    bx0 = min(bx0, s_red[0][w]);
+    by0 = min(by0, s_red[1][w]);
+    bx1 = max(bx1, s_red[2][w]);
+    by1 = max(by1, s_red[3][w]);
+  }
+  const uint32_t rw = bx1 > bx0 ? bx1 - bx0 : 0u, rh = by1 > by0 ? by1 - by0 : 0u, nt = rw * rh;
+  for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_WG) s_hist[k] = 0;
+  // the rects and the inclusive scan of their areas for the workgroup walk
+  const uint32_t area = yh ? (xw >> 16) * (yh >> 16) : 0u;
+  const uint32_t incl = wave_incl_scan(area);
+  __syncthreads();  // (every wave has read s_red)
+  if (lane == 63) s_red[0][wave] = incl;
+  if (threadIdx.x < GS_FUSED_THREADS) s_e[threadIdx.x] = make_uint4(xw, yh, o, __float_as_uint(d));
+  __syncthreads();
+  {
+    uint32_t run = incl;
+    for (uint32_t w = 0; w < wave; ++w) run += s_red[0][w];
+    if (threadIdx.x < GS_FUSED_THREADS) s_incl[threadIdx.x] = run;
+  }
+  __syncthreads();
+  const uint32_t P = s_incl[GS_FUSED_THREADS - 1];
+  STAMP(0, 1);
   STAMP_SYNC();
   STAMP(0, 2);
-  const bool any = __ballot(yh != 0u) != 0ull;
-  if (any)
-    gs_expand<false>(lane, i, xw, yh, 0.0f, [&](uint32_t, uint32_t x, uint32_t y, float) {
-      atomicAdd(s_hist + (y - ty0) * bg.grid_x + x, 1u);
-    });
+  gs_wg_walk(s_incl, s_e, GS_FUSED_THREADS, P, [&](uint32_t, uint32_t x, uint32_t y, uint32_t) {
+    atomicAdd(s_hist + (y - by0) * rw + (x - bx0), 1u);
+  });
   __syncthreads();
   STAMP(0, 3);
-  // reserve: one returning atomic per touched tile; the LDS entry becomes the run's base
+  // reserve: one returning atomic per touched tile (all of a work-item's issued before any is used);
+  // the LDS entry becomes the run's base
   uint32_t pairs = 0, res = 0;
-  for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_THREADS) {
-    const uint32_t c = s_hist[k];
-    if (c) {
-      const uint32_t base = atomicAdd(cursor + t0 + k, c);
-      s_hist[k] = base;
-      pairs += c;
+  const float rcp_rw = 1.0f / (float)max(rw, 1u);
+  for (uint32_t k0 = threadIdx.x; k0 < nt; k0 += 4 * GS_FUSED_WG) {
+    uint32_t c[4], t[4], base[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t k = k0 + j * GS_FUSED_WG;
+      c[j] = k < nt ? s_hist[k] : 0u;
+      uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13 * 2^13: exact after the fix-ups
+      ry = ry * rw > k ? ry - 1 : ry;
+      ry = (ry + 1) * rw <= k ? ry + 1 : ry;
+      t[j] = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) base[j] = c[j] ? atomicAdd(cursor + t[j], c[j]) : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!c[j]) continue;
+      s_hist[k0 + j * GS_FUSED_WG] = base[j];
+      pairs += c[j];
       ++res;
-      if (base + c > scap) __hip_atomic_store(fz + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (base + c > 256u) {
-        atomicMax(fz + 1, base + c);
-        if (base <= GS_MID && base + c > GS_MID) atomicAdd(fz + 4, 1u);  // (one crossing per tile)
+      if (base[j] + c[j] > scap) __hip_atomic_store(fz + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (base[j] + c[j] > 256u) {
+        atomicMax(fz + 1, base[j] + c[j]);
+        if (base[j] <= GS_MID && base[j] + c[j] > GS_MID) atomicAdd(fz + 4, 1u);  // (one crossing per tile)
       }
     }
   }
@@ -726,7 +823,7 @@ __global__ __launch_bounds__(GS_FUSED_THREADS) void gs_bin_fused_kernel(SplatCam
   __syncthreads();
   if (threadIdx.x == 0) {  // per-workgroup partials (the blend's block (0, 0) sums them: no fan-in atomics)
     uint32_t p = 0, r = 0;
-    for (uint32_t w = 0; w < GS_FUSED_THREADS / 64; ++w) {
+    for (uint32_t w = 0; w < GS_FUSED_WG / 64; ++w) {
       p += s_red[0][w];
       r += s_red[1][w];
     }
@@ -735,18 +832,11 @@ __global__ __launch_bounds__(GS_FUSED_THREADS) void gs_bin_fused_kernel(SplatCam
     fzp[2 * wg + 1] = r;
   }
   STAMP(0, 4);
-#ifdef GS_STAMP
-  {
-#else
-  if (!any) return;
-#endif
-  gs_expand<true>(lane, o, xw, yh, d, [&](uint32_t g, uint32_t x, uint32_t y, float dep) {
-    const uint32_t t = y * bg.grid_x + x;
-    const uint32_t rel = atomicAdd(s_hist + (t - t0), 1u);
-    if (rel < scap) tile_slots[(size_t)t * scap + rel] = ((unsigned long long)__float_as_uint(dep) << 32) | g;
+  gs_wg_walk(s_incl, s_e, GS_FUSED_THREADS, P, [&](uint32_t g, uint32_t x, uint32_t y, uint32_t dep) {
+    const uint32_t rel = atomicAdd(s_hist + (y - by0) * rw + (x - bx0), 1u);
+    if (rel < scap) tile_slots[(size_t)(y * bg.grid_x + x) * scap + rel] = ((unsigned long long)dep << 32) | g;
   });
 #ifdef GS_STAMP
-  }
   STAMP_SYNC();
   STAMP(0, 5);
 #endif
@@ -1725,7 +1815,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     BinGrid fg = bgrid;
     fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
     fg.chunk = GS_FUSED_THREADS;
-    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks), dim3(GS_FUSED_THREADS), band_lds, s, cam, fpa, fg,
+    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks), dim3(GS_FUSED_WG), band_lds, s, cam, fpa, fg,
                        scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
                        (unsigned long long*)w->tile_slots.p);
     if ((e2 = hipGetLastError())) return e2;
