@@ -29,6 +29,8 @@ def main():
         order = np.argsort(code, kind="stable")
         g = {k: np.ascontiguousarray(v[order]) for k, v in g.items()}
     dg = {k: torch.from_numpy(v).cuda() for k, v in g.items()}
+    if os.environ.get("GS_SORTED", "0") == "2":  # device Morton sort with ids (renders like the generated order)
+        dg = Renderer(0).sort_gaussians_spatial(dg)
     ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), cornell_box_scene(), 0)
     img = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
     # rotate the order per call (GS_ROUND): the second library loaded in one process measured ~3% faster

@@ -59,7 +59,7 @@ def main():
     if f[:, 0].any() and f[:, 0].min() > 0 and abs(int(f[:, 0].min()) - int(b[:, 0].min())) < 10_000_000:
         print(f"fused front end: {chunks} workgroups, span {(f[:, 5].max() - f[:, 0].min()) * 0.01:.2f} us, "
               f"last start {(f[:, 0].max() - f[:, 0].min()) * 0.01:.2f} us after the first")
-        for k, nm in enumerate(["zero LDS", "preprocess", "count walk", "reserve (atomics)", "scatter walk"]):
+        for k, nm in enumerate(["preprocess + rect + scan", "(sync)", "count walk", "reserve (atomics)", "scatter walk"]):
             stats(nm, f[:, k + 1] - f[:, k])
         stats("workgroup total", f[:, 5] - f[:, 0])
         print(f"  gap fused end -> first blend start {(b[:, 0].min() - f[:, 5].max()) * 0.01:.2f} us")
