@@ -27,8 +27,13 @@ HOST_SOURCES = {"gltf.cpp", "image_decode.cpp", "ply.cpp", "sampling.cpp", "capt
 # per-source extra flags. pt_kernels.hip: SimplifyCFG's common-store sinking merges stores to
 # different Payload fields from the branches of closest_hit into one store through a phi of
 # addresses, which SROA cannot split: the payload then stays a private (scratch) object.
+# pt_wavefront.hip: the SLP vectorizer's horizontal-reduction seeding (-slp-vectorize-hor) turns the
+# extend kernel's loop-carried ray-state phis into <2 x float> phis and, with the textured any-hit
+# inlined, changes the traced rays (opt-bisect: slp-vectorizer on pt_wf_extend_kernel<false, true>;
+# DESIGN.md §4 "-O3 any-hit miscompile", tools/ah_repro.py, tools/ah_variants.py). Without that seeding
+# the inlined any-hit is bit-exact, so the any-hit is no longer called out of line.
 EXTRA = {"pt_kernels.hip": ["-mllvm", "-simplifycfg-sink-common=false"],
-         "pt_wavefront.hip": ["-mllvm", "-simplifycfg-sink-common=false"]}
+         "pt_wavefront.hip": ["-mllvm", "-simplifycfg-sink-common=false", "-mllvm", "-slp-vectorize-hor=false"]}
 ARCH = os.environ.get("PTGS_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC]

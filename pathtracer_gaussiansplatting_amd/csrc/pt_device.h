@@ -173,10 +173,11 @@ __device__ __forceinline__ bool anyhit_accept(const DevScene& sc, uint32_t mesh,
   return !(alpha_hash(seed, gid) > alpha);
 }
 
-// Out-of-line any-hit for the textured wavefront extend kernel: inlined into its refill loop, the
-// textured any-hit (indices -> vertices -> texture alpha) was miscompiled at -O3 (transparent
-// candidates decided differently from pt_camera_kernel / the oracle; bit-exact with this call, at
-// -O1, or with trace_closest called per ray). Only candidates on non-opaque triangles pay the call.
+// Out-of-line any-hit (PTGS_WF_AH_CALL=true builds of pt_wavefront.hip). Round 2 used it to sidestep
+// a miscompile of the inlined textured any-hit in the wavefront extend kernel; root-caused in round 3
+// (opt-bisect): the SLP vectorizer's horizontal-reduction seeding vectorizes the refill loop's
+// ray-state phis and changes the traced rays; build.py compiles pt_wavefront.hip with
+// -slp-vectorize-hor=false and inlines the any-hit.
 __device__ __noinline__ bool anyhit_accept_call(const DevScene& sc, uint32_t mesh, uint32_t prim, float u, float v,
                                                 uint32_t seed, uint32_t gid) {
   return anyhit_accept<true>(sc, mesh, prim, u, v, seed, gid);

@@ -120,7 +120,9 @@ __device__ __forceinline__ void ss_fill(SlotStream& s, const uint8_t* __restrict
 // by work-item, as pt_device.h), deeper entries (rare: C3's tree needs up to 34, C5's 38) in a
 // per-work-item global overflow area. A shorter LDS stack buys occupancy (LDS-bound otherwise).
 #ifndef PTGS_WF_AH_CALL
-#define PTGS_WF_AH_CALL true  // textured any-hit out of line (pt_device.h anyhit_accept_call)
+// textured any-hit inlined (true: out of line, pt_device.h anyhit_accept_call — round 2's workaround for
+// the SLP miscompile that build.py now avoids with -slp-vectorize-hor=false)
+#define PTGS_WF_AH_CALL false
 #endif
 #ifndef PTGS_WF_AH_CALL_EXT
 #define PTGS_WF_AH_CALL_EXT PTGS_WF_AH_CALL

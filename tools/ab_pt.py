@@ -29,6 +29,8 @@ def main():
         path = os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", "libptgs.so" if v == "base" else f"libptgs_{v}.so")
         r = Renderer(0, lib_path=path)
         r.upload_scene(scene)
+        if os.environ.get("AB_WF", "0") == "1":  # the wavefront tracer (PTGS_FLAG_PT_WAVEFRONT)
+            r.set_wavefront(True)
         rs[v] = r
     acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
     res = {v: [] for v in variants}
