@@ -638,7 +638,7 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
 // sequence, [4] tiles above GS_MID pairs; per workgroup fzp: (pairs, reservations); published to the
 // host by the blend's block (0, 0).
 #ifndef GS_FUSED_THREADS
-#define GS_FUSED_THREADS 512
+#define GS_FUSED_THREADS 256  // Gaussians per fused workgroup (512 / 1 024 work-items: 1.5 us slower at C2)
 #endif
 struct GsFused {  // the sort's and the blend's view of a fused-front-end frame (scap == 0: three-launch path)
   uint32_t scap, seq;
@@ -667,7 +667,7 @@ __device__ unsigned long long g_gs_stamps[2][GS_STAMP_WG * GS_STAMP_N];
 #define STAMP_SYNC() do { } while (0)
 #endif
 #ifndef GS_FUSED_WG
-#define GS_FUSED_WG 1024  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
+#define GS_FUSED_WG 512  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
 #endif
 
 // Workgroup-cooperative pair walk of the fused front end: the chunk's rects (s_e: x0 | w << 16,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Build libptgs_<name>.so variants whose pt_wavefront.hip object gets extra compiler flags (for the
-any-hit inlining investigation, tools/ah_repro.py): name=flag,flag,... ; the other objects are the
-default ones (shared per variant directory).
+"""Build libptgs_<name>.so variants whose pt_wavefront.hip object (or name@<source>) gets extra compiler
+flags (the any-hit inlining investigation, tools/ah_repro.py; compiler-flag A/B of a kernel file):
+name[@source]=flag,flag,... ; the other objects are the default ones.
    tools/ah_variants.py ahinl_b6481=-DPTGS_WF_AH_CALL=false,-mllvm,-opt-bisect-limit=6481 ..."""
 import os
 import subprocess
@@ -15,12 +15,15 @@ def main():
     from pathtracer_gaussiansplatting_amd import build as B
     for spec in sys.argv[1:]:
         name, flags = spec.split("=", 1)
+        src = "pt_wavefront.hip"
+        if "@" in name:  # name@source.hip=flags: another source file
+            name, src = name.split("@", 1)
         flags = flags.split(",") if flags else []
         bdir = B.BUILD + "_" + name
         os.makedirs(bdir, exist_ok=True)
-        obj = os.path.join(bdir, "pt_wavefront.hip.o")
-        cmd = ([B._hipcc()] + B.COMMON + B.EXTRA["pt_wavefront.hip"] + flags +
-               [f"--offload-arch={B.ARCH}", "-c", os.path.join(B.CSRC, "pt_wavefront.hip"), "-o", obj])
+        obj = os.path.join(bdir, src + ".o")
+        cmd = ([B._hipcc()] + B.COMMON + B.EXTRA.get(src, []) + flags +
+               [f"--offload-arch={B.ARCH}", "-c", os.path.join(B.CSRC, src), "-o", obj])
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode:
             print(name, "FAILED", r.stderr[-2000:])
