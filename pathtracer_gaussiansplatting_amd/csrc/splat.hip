@@ -64,12 +64,8 @@ struct SplatWorkspace {
   bool hint_recorded = false;
   hipEvent_t hint_event = nullptr;
   bool last_fused = false;    // the last frame ran the fused front end
-  // front-end policy: 0 fused, 1 probing (one fused frame, seq fe_probe, until its result is in),
-  // 2 three launches for fe_hold more frames
-  uint32_t fe_state = 1, fe_probe = 0, fe_hold = 0;
   uint32_t* k_host = nullptr;  // pinned, coherent [16]: K, largest tile, large tiles, skipped frames,
-                               // touched runs, fused overflow, publishing path (1 fused / 2 three),
-                               // latest fused frame's seq, its runs
+                               // touched runs, fused overflow, publishing path (1 fused / 2 three)
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
@@ -1227,10 +1223,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       __atomic_store_n(fu.k_host + 1, big > 256u ? big : 256u, __ATOMIC_RELAXED);  // largest tile (bound)
       __atomic_store_n(fu.k_host + 2, fu.fz[4], __ATOMIC_RELAXED);                  // large tiles
       __atomic_store_n(fu.k_host + 4, fr, __ATOMIC_RELAXED);                        // reservations
-      __atomic_store_n(fu.k_host + 8, fr, __ATOMIC_RELAXED);                        // (the policy's copy)
       __atomic_store_n(fu.k_host + 5, ovf ? 1u : 0u, __ATOMIC_RELAXED);            // tile above scap
       __atomic_store_n(fu.k_host + 6, 1u, __ATOMIC_RELAXED);                       // published by: fused
-      __atomic_store_n(fu.k_host + 7, fu.seq, __ATOMIC_RELAXED);                   // ... this frame
       if (ovf) __atomic_store_n(fu.k_host + 3, __atomic_load_n(fu.k_host + 3, __ATOMIC_RELAXED) + 1u, __ATOMIC_RELAXED);
       __atomic_store_n(fu.k_host, fp, __ATOMIC_RELAXED);
       fu.fz[1] = 0;
@@ -1731,38 +1725,20 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
 #ifndef GS_FUSED_RUNS_PER_TILE
 #define GS_FUSED_RUNS_PER_TILE 16u
 #endif
-  // policy (PTGS_GS_FRONTEND unset): the fused path while its frames reserve at most
-  // GS_FUSED_RUNS_PER_TILE runs per tile (Gaussians in a spatially coherent order: each workgroup
-  // touches a compact set of tiles; in random order every workgroup touches most tiles and the
-  // reservations cost more than the histograms); otherwise three launches for 128 frames, then a probe
+  // policy (PTGS_GS_FRONTEND unset): the fused path while frames touch at most
+  // GS_FUSED_RUNS_PER_TILE (workgroup, tile) runs per tile (Gaussians in a spatially coherent order:
+  // each workgroup touches a compact set of tiles; in random order every workgroup touches most tiles
+  // and the reservations cost more than the histograms), else three launches
   static const int frontend = [] {
     const char* v = getenv("PTGS_GS_FRONTEND");  // "fused" / "three" (A/B switch)
     if (v && !strcmp(v, "three")) return 0;
     if (v && !strcmp(v, "fused")) return 1;
     return GS_FRONTEND_DEFAULT ? 2 : 0;
   }();
-  // (a fused frame's runs reach the host asynchronously (k_host[4], tagged with its seq in k_host[7]):
-  // after a probe, frames use three launches until its result is in; a passing probe keeps the fused
-  // path, and each later fused result is checked again)
-  bool want_fused = frontend == 1;
-  if (frontend == 2) {
-    // k_host[7] / [8]: seq and runs of the latest fused frame (a three-launch frame does not touch them)
-    const bool result_in = w->k_host[7] == w->fe_probe;
-    const bool coherent = w->k_host[8] <= GS_FUSED_RUNS_PER_TILE * tiles;
-    if (w->fe_state == 0) {  // fused: re-checked on every fused result
-      if (w->k_host[7] && !coherent) {
-        w->fe_state = 2;
-        w->fe_hold = 128;
-      }
-    } else if (w->fe_state == 1 && w->fe_probe && result_in) {  // probing: the probe's result is in
-      w->fe_state = coherent ? 0 : 2;
-      w->fe_hold = coherent ? 0 : 128;
-    } else if (w->fe_state == 2 && --w->fe_hold == 0) {  // held: probe again
-      w->fe_state = 1;
-      w->fe_probe = 0;
-    }
-    want_fused = w->fe_state == 0 || (w->fe_state == 1 && w->fe_probe == 0);
-  }
+  // both front ends publish the frame's touched (workgroup, tile) runs (k_host[4]: the fused kernel's
+  // reservations, the count kernel's nonzero histogram entries); the latest one decides, so the
+  // choice is made from the first finished frame on and follows the data's coherence both ways
+  const bool want_fused = frontend == 1 || (frontend == 2 && w->k_host[4] <= GS_FUSED_RUNS_PER_TILE * tiles);
   uint32_t scap = 0;
   if (want_fused && w->have_hint && n) {
     const uint32_t big = std::max(256u, w->k_host[1] + w->k_host[1] / 4u);
@@ -1806,7 +1782,6 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     const uint32_t nwg = bgrid.bands * ((n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS);
     if ((e2 = ensure(w->fzp, (size_t)nwg * 8))) return e2;
     const uint32_t seq = ++w->seq;
-    if (w->fe_state == 1 && w->fe_probe == 0) w->fe_probe = seq;
     GsFused fu = {scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
                   (uint32_t*)w->fzp.p, nwg};
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers

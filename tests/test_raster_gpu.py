@@ -362,30 +362,34 @@ def test_gaussians_fused_front_end(native_lib, oracle_lib, n, W, H):
 
 
 def test_gaussians_front_end_policy(native_lib, oracle_lib):
-    """Gaussians in their generated (random) order touch most tiles from every front-end workgroup:
-    the fused probe frame reports > 16 runs per tile and the next frames go back to three launches;
-    every frame is the oracle's."""
+    """Front-end choice from the touched (workgroup, tile) runs both front ends publish: Gaussians in
+    their generated (random) order touch most tiles from every workgroup (> 16 runs per tile): three
+    launches on every frame; the same set in Morton order (ptgs_gaussians_sort_spatial): the fused
+    front end from the second frame on. Every frame is the oracle's."""
     from pathtracer_gaussiansplatting_amd import Renderer
     n, W, H = 100_000, 1920, 1080
     g = Y.gaussians_c2(n, seed=9)
     ubo = _gauss_ubo(W, H)
     ref = oracle_lib.splat_gaussians(g, ubo, W, H)
-    r = Renderer(0, publish_splat_buffers=True)
-    try:
-        dg = {k: _dev(v) for k, v in g.items()}
-        got = []
-        for frame in range(4):
-            out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
-            st = r.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
-            torch.cuda.synchronize()
-            got.append(st.fused)
-            if frame == 1:
+    for order in ("generated", "morton"):
+        r = Renderer(0, publish_splat_buffers=True)
+        try:
+            dg = {k: _dev(v) for k, v in g.items()}
+            if order == "morton":
+                dg = r.sort_gaussians_spatial(dg)
+            got = []
+            for frame in range(3):
+                out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+                st = r.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
+                torch.cuda.synchronize()
+                got.append(st.fused)
                 s = r.splat_status()
-                assert s.fused == 1 and s.touched_runs > 16 * st.tiles_x * st.tiles_y, s.touched_runs
-            _check_published(r, st, ref, out, n, f"frame {frame}")
-        assert got == [0, 1, 0, 0], got
-    finally:
-        r.close()
+                per_tile = s.touched_runs / (st.tiles_x * st.tiles_y)
+                assert (per_tile > 16) == (order == "generated"), (order, per_tile)
+                _check_published(r, st, ref, out, n, f"{order} frame {frame}")
+            assert got == ([0, 0, 0] if order == "generated" else [0, 1, 1]), (order, got)
+        finally:
+            r.close()
 
 
 def test_gaussians_spatial_order_renders_identically(native_lib, oracle_lib):
