@@ -1465,9 +1465,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     // each wave compacts its own quadrant's list from every staged mask, in sorted order (no
     // cross-wave counts: one barrier per batch fewer, two fewer for a small tile)
     const uint32_t nb = min((uint32_t)GS_BLOCK, n - base);
+    const uint32_t nbu = (uint32_t)__builtin_amdgcn_readfirstlane((int)nb);
     uint32_t cnt = 0;
 #pragma unroll
     for (uint32_t k = 0; k < GS_BLOCK / 64; ++k) {
+      if (k * 64u >= nbu) break;  // (uniform: only the rounds that hold staged entries)
       const uint32_t p = k * 64u + lane;
       const uint32_t slot = small ? (uint32_t)s_sslot[p] : p;
       const bool bit = p < nb && ((s_mask[slot] >> wave) & 1u);
