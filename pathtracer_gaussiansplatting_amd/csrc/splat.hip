@@ -58,7 +58,7 @@ struct SplatWorkspace {
   DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, tile_info,
       group_total, tile_slots, point_keys, total, rect, large, large_ctr, sort_scratch;
   DevBuf cursor, fz, pub_offs, keys_pub, vals_pub;  // fused front end (see gs_bin_fused_kernel)
-  DevBuf dbg_depths, fzp, nzbuf;
+  DevBuf dbg_depths, fzp, nzbuf, order;  // order: the blend's tile order (heavy first, fused frames)
   uint32_t seq = 0;           // fused frames enqueued (the overflow word's tag)
   bool have_hint = false;     // a finished frame has published its largest tile: the fused path can size its rows
   bool hint_recorded = false;
@@ -644,6 +644,7 @@ struct GsFused {  // the sort's and the blend's view of a fused-front-end frame 
   uint2* ranges;      // the tile ranges the blend writes (t * scap, t * scap + n)
   uint32_t* fzp;      // per front-end workgroup: (pairs, reservations)
   uint32_t nwg;
+  const uint32_t* order;  // blend workgroup -> tile (heavy tiles first; null: row-major)
 };
 // GS_STAMP builds (tools/gs_stamps.py): per-workgroup s_memrealtime (100 MHz) stamps at phase
 // boundaries of the fused front end and the blend, read back with ptgs_debug_stamps.
@@ -665,6 +666,38 @@ __device__ unsigned long long g_gs_stamps[2][GS_STAMP_WG * GS_STAMP_N];
 #ifndef GS_FUSED_WG
 #define GS_FUSED_WG 512  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
 #endif
+
+// The blend's tile order for a fused frame, built by one extra workgroup of the fused launch while
+// the others bin: the tiles [tb, te) by the previous frame's pair count, heaviest first (a counting
+// sort on min(255, n / 2), descending; the order inside a bucket is the LDS atomics'). The blend's
+// workgroups are dispatched in index order, so its long-running tiles start first and the kernel's
+// ramp-down runs light tiles only. Any permutation renders the same image: the previous frame's
+// counts (ranges[t].y - .x, whatever path wrote them) only steer the schedule.
+#define GS_ORDER_BUCKETS 256u
+static_assert(GS_FUSED_THREADS >= 256, "gs_tile_order's buckets live in s_incl");
+__device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
+  const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
+  return GS_ORDER_BUCKETS - 1u - min(GS_ORDER_BUCKETS - 1u, n >> 1);
+}
+__device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restrict__ order, uint32_t tb, uint32_t te,
+                              uint32_t* s_h /* >= GS_ORDER_BUCKETS */) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  for (uint32_t b = tid; b < GS_ORDER_BUCKETS; b += GS_FUSED_WG) s_h[b] = 0;
+  __syncthreads();
+  for (uint32_t t = tb + tid; t < te; t += GS_FUSED_WG) atomicAdd(s_h + gs_order_bucket(prev[t]), 1u);
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the buckets: one wave, four per lane
+    const uint32_t c0 = s_h[4 * lane], c1 = s_h[4 * lane + 1], c2 = s_h[4 * lane + 2], c3 = s_h[4 * lane + 3];
+    const uint32_t sum = (c0 + c1) + (c2 + c3);
+    const uint32_t ex = wave_incl_scan(sum) - sum;
+    s_h[4 * lane] = ex;
+    s_h[4 * lane + 1] = ex + c0;
+    s_h[4 * lane + 2] = ex + c0 + c1;
+    s_h[4 * lane + 3] = ex + c0 + c1 + c2;
+  }
+  __syncthreads();
+  for (uint32_t t = tb + tid; t < te; t += GS_FUSED_WG) order[atomicAdd(s_h + gs_order_bucket(prev[t]), 1u)] = t;
+}
 
 // Workgroup-cooperative pair walk of the fused front end: the chunk's rects (s_e: x0 | w << 16,
 // y0 | h << 16, key index, depth bits) and the inclusive scan of their areas (s_incl) are in LDS;
@@ -708,11 +741,18 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
                                                                          uint32_t* __restrict__ cursor,
                                                                          uint32_t* __restrict__ fz,
                                                                          uint32_t* __restrict__ fzp,
-                                                                         unsigned long long* __restrict__ tile_slots) {
+                                                                         unsigned long long* __restrict__ tile_slots,
+                                                                         const uint2* __restrict__ prev_ranges,
+                                                                         uint32_t* __restrict__ order,
+                                                                         uint32_t order_tb, uint32_t order_te) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // <= band_rows * grid_x
   __shared__ uint32_t s_red[4][GS_FUSED_WG / 64];
   __shared__ uint32_t s_incl[GS_FUSED_THREADS];
   __shared__ uint4 s_e[GS_FUSED_THREADS];
+  if (order && blockIdx.y == gridDim.y - 1) {  // the extra row of blocks: the blend's tile order
+    if (blockIdx.x == 0) gs_tile_order(prev_ranges, order, order_tb, order_te, s_incl);
+    return;
+  }
   STAMP(0, 0);
   uint32_t ty0, ty1;
   gs_band(bg, ty0, ty1);
@@ -1243,10 +1283,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   // Gaussians they share stay in that XCD's L2
   const uint32_t tl = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const uint32_t tile_x = tl % gridDim.x, tile_y = cam.row_begin + tl / gridDim.x;
-#else
-  const uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
-#endif
   const uint32_t tile = tile_y * cam.grid_x + tile_x;
+#else
+  uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
+  uint32_t tile = tile_y * cam.grid_x + tile_x;
+  if (fu.order) {  // fused frames: heavy tiles first (gs_tile_order)
+    tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)fu.order[blockIdx.y * gridDim.x + blockIdx.x]);
+    tile_y = tile / cam.grid_x;
+    tile_x = tile - tile_y * cam.grid_x;
+  }
+#endif
   const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
   // Stage a record as the quadratic in tile-local pixel coordinates (ux, uy):
   // z = A ux^2 + B ux uy + C uy^2 + D ux + E uy + F (five FMAs per evaluation instead of seven), and
@@ -1724,6 +1770,9 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
 #ifndef GS_FRONTEND_DEFAULT
 #define GS_FRONTEND_DEFAULT 1  // 0: always three launches
 #endif
+#ifndef GS_TILE_ORDER
+#define GS_TILE_ORDER 1  // fused frames blend their tiles heaviest first (gs_tile_order)
+#endif
 #ifndef GS_FUSED_RUNS_PER_TILE
 #define GS_FUSED_RUNS_PER_TILE 16u
 #endif
@@ -1766,7 +1815,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if (!e2) w->sort_attr = true;
     return e2;
   };
-  const GsFused no_fu = {0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u};
+  const GsFused no_fu = {0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, nullptr};
 
   auto enqueue_fused = [&]() -> hipError_t {
     hipError_t e2;
@@ -1784,17 +1833,23 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     const uint32_t nwg = bgrid.bands * ((n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS);
     if ((e2 = ensure(w->fzp, (size_t)nwg * 8))) return e2;
     const uint32_t seq = ++w->seq;
+    uint32_t* order = nullptr;
+#if GS_TILE_ORDER
+    if ((e2 = ensure(w->order, (size_t)tiles * 4))) return e2;
+    if (rows) order = (uint32_t*)w->order.p;
+#endif
     GsFused fu = {scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
-                  (uint32_t*)w->fzp.p, nwg};
+                  (uint32_t*)w->fzp.p, nwg, order};
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers
     fpa.rects = nullptr;
     fpa.depths = nullptr;
     BinGrid fg = bgrid;
     fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
     fg.chunk = GS_FUSED_THREADS;
-    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks), dim3(GS_FUSED_WG), band_lds, s, cam, fpa, fg,
-                       scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
-                       (unsigned long long*)w->tile_slots.p);
+    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks + (order ? 1u : 0u)), dim3(GS_FUSED_WG), band_lds, s,
+                       cam, fpa, fg, scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
+                       (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, order,
+                       cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x);
     if ((e2 = hipGetLastError())) return e2;
     if ((e2 = mark(1)) || (e2 = mark(2)) || (e2 = mark(3))) return e2;
     unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
