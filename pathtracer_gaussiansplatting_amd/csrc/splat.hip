@@ -129,6 +129,23 @@ struct PreArgs {
                         // per-Gaussian outputs use it, so a reordered set renders like the original
 };
 
+// Stores that may stream past L2 (A/B: GS_NT_REC for the blend records, GS_NT_OUT for the image)
+template <bool NT>
+__device__ __forceinline__ void gs_st4(float4* p, const float4& v) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  if (NT) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
+  else *p = v;
+}
+#ifndef GS_NT_REC
+#define GS_NT_REC 0
+#endif
+#ifndef GS_NT_OUT
+#define GS_NT_OUT 1  // image stores stream out: C2 0.0686 -> 0.0677 ms (fewer dirty lines at the kernel end)
+#endif
+#ifndef GS_NT_SLOTS
+#define GS_NT_SLOTS 0
+#endif
+
 // One Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T, EWA Sigma' = J W Sigma W^T J^T + 0.3,
 // conic, 3-sigma radius, tile rect (returned; empty if culled) and, with STORE, every per-Gaussian
 // output incl. the blend record. (Blocks of other bands recompute the rect without storing.)
@@ -160,6 +177,20 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
     if (rects) rects[i] = none;  // empty rect: the scatter reads rects only
   }
   float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
+  // every input is loaded here, before the depth test: one memory round trip per Gaussian (loads
+  // behind the test's branch were issued only once the means had arrived)
+  float qr = rots[4 * i], qx = rots[4 * i + 1], qy = rots[4 * i + 2], qz = rots[4 * i + 3];
+  float sx = scales[3 * i], sy = scales[3 * i + 1], sz = scales[3 * i + 2];
+  float op = opac[i];
+  float cr = 0.0f, cg = 0.0f, cbl = 0.0f;
+  if (STORE) {
+    cr = colors[3 * i];
+    cg = colors[3 * i + 1];
+    cbl = colors[3 * i + 2];
+    asm volatile("" : "+v"(cr), "+v"(cg), "+v"(cbl));
+  }
+  // (the empty asm needs the values here, so the compiler cannot sink the loads behind the branch)
+  asm volatile("" : "+v"(qr), "+v"(qx), "+v"(qy), "+v"(qz), "+v"(sx), "+v"(sy), "+v"(sz), "+v"(op));
   // frustum: view-space depth d = -z (RH, camera looks down -Z)
   v4 pv = mv4(cam.view, mx, my, mz, 1.0f);
   float d = -pv.z;
@@ -170,10 +201,8 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   float px = ph.x * pw, py = ph.y * pw;
 
   // Sigma = R S^2 R^T
-  float qr = rots[4 * i], qx = rots[4 * i + 1], qy = rots[4 * i + 2], qz = rots[4 * i + 3];
   float qn = sqrtx(((qr * qr + qx * qx) + qy * qy) + qz * qz);
   qr = qr / qn; qx = qx / qn; qy = qy / qn; qz = qz / qn;
-  float sx = scales[3 * i], sy = scales[3 * i + 1], sz = scales[3 * i + 2];
   float R00 = 1.0f - 2.0f * (qy * qy + qz * qz), R01 = 2.0f * (qx * qy - qr * qz), R02 = 2.0f * (qx * qz + qr * qy);
   float R10 = 2.0f * (qx * qy + qr * qz), R11 = 1.0f - 2.0f * (qx * qx + qz * qz), R12 = 2.0f * (qy * qz - qr * qx);
   float R20 = 2.0f * (qx * qz - qr * qy), R21 = 2.0f * (qy * qz + qr * qx), R22 = 1.0f - 2.0f * (qx * qx + qy * qy);
@@ -211,7 +240,7 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   float det = ca * cc - cb * cb;
   if (det == 0.0f) return none;
   float det_inv = 1.0f / det;
-  float4 con = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, opac[i]);
+  float4 con = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, op);
   float mid = 0.5f * (ca + cc);
   float disc = sqrtx(fmaxx(0.1f, mid * mid - det));
   float l1 = mid + disc, l2 = mid - disc;
@@ -250,9 +279,9 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   const float sq = -2.0f * skip;
   const float ex = sq > 0.0f ? sqrtx(sq * ca) * 1.01f + 0.01f : -1.0f;
   const float ey = sq > 0.0f ? sqrtx(sq * cc) * 1.01f + 0.01f : -1.0f;
-  rec[3 * o] = make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E);
-  rec[3 * o + 1] = make_float4(-0.5f * con.z * L2E, __log2f(con.w), colors[3 * i], colors[3 * i + 1]);
-  rec[3 * o + 2] = make_float4(colors[3 * i + 2], ex, ey, d);
+  gs_st4<GS_NT_REC>(rec + 3 * o, make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E));
+  gs_st4<GS_NT_REC>(rec + 3 * o + 1, make_float4(-0.5f * con.z * L2E, __log2f(con.w), cr, cg));
+  gs_st4<GS_NT_REC>(rec + 3 * o + 2, make_float4(cbl, ex, ey, d));
   return rect;
 }
 
@@ -400,13 +429,55 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
   }
 }
 
+// The blend's tile order, built by one extra workgroup of the front end's first launch (fused or
+// count) while the others bin: the tiles [tb, te) by the previous frame's pair count, heaviest first (a counting
+// sort on min(255, n / 2), descending; the order inside a bucket is the LDS atomics'). The blend's
+// workgroups are dispatched in index order, so its long-running tiles start first and the kernel's
+// ramp-down runs light tiles only. Any permutation renders the same image: the previous frame's
+// counts (ranges[t].y - .x, whatever path wrote them) only steer the schedule.
+#define GS_ORDER_BUCKETS 256u
+__device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
+  const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
+  return GS_ORDER_BUCKETS - 1u - min(GS_ORDER_BUCKETS - 1u, n >> 1);
+}
+__device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restrict__ order, uint32_t tb, uint32_t te,
+                              uint32_t* s_h /* >= GS_ORDER_BUCKETS */) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, nth = blockDim.x;  // (>= 64)
+  for (uint32_t b = tid; b < GS_ORDER_BUCKETS; b += nth) s_h[b] = 0;
+  __syncthreads();
+  for (uint32_t t = tb + tid; t < te; t += nth) atomicAdd(s_h + gs_order_bucket(prev[t]), 1u);
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the buckets: one wave, four per lane
+    const uint32_t c0 = s_h[4 * lane], c1 = s_h[4 * lane + 1], c2 = s_h[4 * lane + 2], c3 = s_h[4 * lane + 3];
+    const uint32_t sum = (c0 + c1) + (c2 + c3);
+    const uint32_t ex = wave_incl_scan(sum) - sum;
+    s_h[4 * lane] = ex;
+    s_h[4 * lane + 1] = ex + c0;
+    s_h[4 * lane + 2] = ex + c0 + c1;
+    s_h[4 * lane + 3] = ex + c0 + c1 + c2;
+  }
+  __syncthreads();
+#ifdef GS_ORDER_IDENTITY  // (A/B probe: the blend's extra load without the reordering)
+  for (uint32_t t = tb + tid; t < te; t += nth) order[t - tb] = t;
+  return;
+#endif
+  for (uint32_t t = tb + tid; t < te; t += nth) order[atomicAdd(s_h + gs_order_bucket(prev[t]), 1u)] = t;
+}
+
 // preprocess + count. Block (0, 0) also re-arms the frame's counters.
 __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                       uint32_t* __restrict__ hist,
                                                                       uint32_t* __restrict__ total,
                                                                       uint32_t* __restrict__ large_ctr,
-                                                                      uint32_t* k_host, uint32_t* __restrict__ nzbuf) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x
+                                                                      uint32_t* k_host, uint32_t* __restrict__ nzbuf,
+                                                                      const uint2* __restrict__ prev_ranges,
+                                                                      uint32_t* __restrict__ order, uint32_t order_tb,
+                                                                      uint32_t order_te) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x (>= GS_ORDER_BUCKETS)
+  if (order && blockIdx.y == gridDim.y - 1) {  // the extra row of blocks: the blend's tile order
+    if (blockIdx.x == 0) gs_tile_order(prev_ranges, order, order_tb, order_te, s_hist);
+    return;
+  }
   uint32_t ty0, ty1;
   gs_band(bg, ty0, ty1);
   const uint32_t nt = (ty1 - ty0) * bg.grid_x;
@@ -667,38 +738,6 @@ __device__ unsigned long long g_gs_stamps[2][GS_STAMP_WG * GS_STAMP_N];
 #define GS_FUSED_WG 512  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
 #endif
 
-// The blend's tile order for a fused frame, built by one extra workgroup of the fused launch while
-// the others bin: the tiles [tb, te) by the previous frame's pair count, heaviest first (a counting
-// sort on min(255, n / 2), descending; the order inside a bucket is the LDS atomics'). The blend's
-// workgroups are dispatched in index order, so its long-running tiles start first and the kernel's
-// ramp-down runs light tiles only. Any permutation renders the same image: the previous frame's
-// counts (ranges[t].y - .x, whatever path wrote them) only steer the schedule.
-#define GS_ORDER_BUCKETS 256u
-static_assert(GS_FUSED_THREADS >= 256, "gs_tile_order's buckets live in s_incl");
-__device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
-  const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
-  return GS_ORDER_BUCKETS - 1u - min(GS_ORDER_BUCKETS - 1u, n >> 1);
-}
-__device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restrict__ order, uint32_t tb, uint32_t te,
-                              uint32_t* s_h /* >= GS_ORDER_BUCKETS */) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  for (uint32_t b = tid; b < GS_ORDER_BUCKETS; b += GS_FUSED_WG) s_h[b] = 0;
-  __syncthreads();
-  for (uint32_t t = tb + tid; t < te; t += GS_FUSED_WG) atomicAdd(s_h + gs_order_bucket(prev[t]), 1u);
-  __syncthreads();
-  if (tid < 64) {  // exclusive scan of the buckets: one wave, four per lane
-    const uint32_t c0 = s_h[4 * lane], c1 = s_h[4 * lane + 1], c2 = s_h[4 * lane + 2], c3 = s_h[4 * lane + 3];
-    const uint32_t sum = (c0 + c1) + (c2 + c3);
-    const uint32_t ex = wave_incl_scan(sum) - sum;
-    s_h[4 * lane] = ex;
-    s_h[4 * lane + 1] = ex + c0;
-    s_h[4 * lane + 2] = ex + c0 + c1;
-    s_h[4 * lane + 3] = ex + c0 + c1 + c2;
-  }
-  __syncthreads();
-  for (uint32_t t = tb + tid; t < te; t += GS_FUSED_WG) order[atomicAdd(s_h + gs_order_bucket(prev[t]), 1u)] = t;
-}
-
 // Workgroup-cooperative pair walk of the fused front end: the chunk's rects (s_e: x0 | w << 16,
 // y0 | h << 16, key index, depth bits) and the inclusive scan of their areas (s_incl) are in LDS;
 // work-item t takes the contiguous pairs [t q, t q + q) of the chunk's P (q = ceil(P / GS_FUSED_WG)):
@@ -736,6 +775,58 @@ __device__ __forceinline__ void gs_wg_walk(const uint32_t* s_incl, const uint4* 
   }
 }
 
+// The count walk of a chunk with at most GS_FUSED_QREG pairs per work-item: the same walk as
+// gs_wg_walk, with returning LDS atomics whose results (the pair's rank among the chunk's pairs of its
+// tile) are kept in registers with the pair, packed as k | rank << 13 | j << 21 (k: tile in the
+// chunk's rect, < 8192 = GS_BAND_TILES; rank < 256: one pair per Gaussian and tile; j: Gaussian in the
+// chunk, < 256). The scatter then writes each kept pair at its run's base + rank without walking the
+// rects again or touching an LDS atomic. Returns the work-item's pair count.
+#ifndef GS_FUSED_QREG
+#define GS_FUSED_QREG 16  // (C2 needs <= 7; 8 and 16 measured equal: 50 / 53 VGPRs)
+#endif
+#ifndef GS_FUSED_KEEP
+#define GS_FUSED_KEEP 1
+#endif
+static_assert(GS_FUSED_THREADS <= 256 && GS_BAND_TILES <= 8192, "gs_wg_count_keep's packing");
+__device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, const uint4* s_e, uint32_t ng, uint32_t P,
+                                                     uint32_t* s_hist, uint32_t bx0, uint32_t by0, uint32_t rw,
+                                                     uint32_t (&pk)[GS_FUSED_QREG]) {
+  const uint32_t q = (P + GS_FUSED_WG - 1) / GS_FUSED_WG;
+  uint32_t p = threadIdx.x * q;
+  const uint32_t p1 = min(P, p + q);
+  if (p >= p1) return 0;
+  const uint32_t cnt = p1 - p;
+  uint32_t lo = 0, hi = ng - 1;  // first j with incl[j] > p
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s_incl[mid] > p) hi = mid;
+    else lo = mid + 1;
+  }
+  uint32_t j = lo;
+  uint4 e = s_e[j];
+  uint32_t w = e.x >> 16, r = p - (s_incl[j] - w * (e.y >> 16));
+  uint32_t ry = r / w, rx = r - ry * w;
+#pragma unroll
+  for (uint32_t c = 0; c < GS_FUSED_QREG; ++c) {
+    if (c < cnt) {
+      const uint32_t k = ((e.y & 0xFFFFu) + ry - by0) * rw + ((e.x & 0xFFFFu) + rx - bx0);
+      const uint32_t rank = atomicAdd(s_hist + k, 1u);
+      pk[c] = k | (rank << 13) | (j << 21);
+      if (c + 1 < cnt && ++rx == w) {
+        rx = 0;
+        if (++ry == (e.y >> 16)) {  // next rect with pairs
+          do {
+            e = s_e[++j];
+          } while ((e.y >> 16) == 0u || (e.x >> 16) == 0u);
+          w = e.x >> 16;
+          ry = 0;
+        }
+      }
+    }
+  }
+  return cnt;
+}
+
 __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                          uint32_t scap, uint32_t seq,
                                                                          uint32_t* __restrict__ cursor,
@@ -749,6 +840,7 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
   __shared__ uint32_t s_red[4][GS_FUSED_WG / 64];
   __shared__ uint32_t s_incl[GS_FUSED_THREADS];
   __shared__ uint4 s_e[GS_FUSED_THREADS];
+  static_assert(GS_FUSED_THREADS >= GS_ORDER_BUCKETS, "gs_tile_order's buckets live in s_incl");
   if (order && blockIdx.y == gridDim.y - 1) {  // the extra row of blocks: the blend's tile order
     if (blockIdx.x == 0) gs_tile_order(prev_ranges, order, order_tb, order_te, s_incl);
     return;
@@ -813,9 +905,17 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
   STAMP(0, 1);
   STAMP_SYNC();
   STAMP(0, 2);
-  gs_wg_walk(s_incl, s_e, GS_FUSED_THREADS, P, [&](uint32_t, uint32_t x, uint32_t y, uint32_t) {
-    atomicAdd(s_hist + (y - by0) * rw + (x - bx0), 1u);
-  });
+  // (uniform) pairs kept in registers between the count and the scatter, or a second walk
+  const bool keep = GS_FUSED_KEEP && P <= (uint32_t)GS_FUSED_WG * GS_FUSED_QREG;
+  uint32_t pk[GS_FUSED_QREG];
+  uint32_t kept = 0;
+  if (keep) {
+    kept = gs_wg_count_keep(s_incl, s_e, GS_FUSED_THREADS, P, s_hist, bx0, by0, rw, pk);
+  } else {
+    gs_wg_walk(s_incl, s_e, GS_FUSED_THREADS, P, [&](uint32_t, uint32_t x, uint32_t y, uint32_t) {
+      atomicAdd(s_hist + (y - by0) * rw + (x - bx0), 1u);
+    });
+  }
   __syncthreads();
   STAMP(0, 3);
   // reserve: one returning atomic per touched tile (all of a work-item's issued before any is used);
@@ -868,9 +968,33 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
     fzp[2 * wg + 1] = r;
   }
   STAMP(0, 4);
+  if (keep) {  // (every run's base is in s_hist: the barrier before the partials' sum)
+#pragma unroll
+    for (uint32_t c = 0; c < GS_FUSED_QREG; ++c) {
+      if (c < kept) {
+        const uint32_t k = pk[c] & 0x1FFFu, rel = s_hist[k] + ((pk[c] >> 13) & 0xFFu);
+        const uint4 e = s_e[pk[c] >> 21];
+        uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13: exact after the fix-ups
+        ry = ry * rw > k ? ry - 1 : ry;
+        ry = (ry + 1) * rw <= k ? ry + 1 : ry;
+        const uint32_t t = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
+        if (rel < scap) {
+          const unsigned long long key = ((unsigned long long)e.w << 32) | e.z;
+          unsigned long long* dst = tile_slots + (size_t)t * scap + rel;
+          if (GS_NT_SLOTS) __builtin_nontemporal_store(key, dst);
+          else *dst = key;
+        }
+      }
+    }
+  } else
   gs_wg_walk(s_incl, s_e, GS_FUSED_THREADS, P, [&](uint32_t g, uint32_t x, uint32_t y, uint32_t dep) {
     const uint32_t rel = atomicAdd(s_hist + (y - by0) * rw + (x - bx0), 1u);
-    if (rel < scap) tile_slots[(size_t)(y * bg.grid_x + x) * scap + rel] = ((unsigned long long)dep << 32) | g;
+    if (rel < scap) {
+      const unsigned long long key = ((unsigned long long)dep << 32) | g;
+      unsigned long long* dst = tile_slots + (size_t)(y * bg.grid_x + x) * scap + rel;
+      if (GS_NT_SLOTS) __builtin_nontemporal_store(key, dst);
+      else *dst = key;
+    }
   });
 #ifdef GS_STAMP
   STAMP_SYNC();
@@ -1586,9 +1710,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const size_t pix = (size_t)py2 * cam.W + px2;
     if (OVER) {
       const float4 u4 = under[pix];
-      out[pix] = make_float4(C0 + T * u4.x, C1 + T * u4.y, C2 + T * u4.z, (1.0f - T) + T * u4.w);
+      gs_st4<GS_NT_OUT>(out + pix, make_float4(C0 + T * u4.x, C1 + T * u4.y, C2 + T * u4.z, (1.0f - T) + T * u4.w));
     } else {
-      out[pix] = make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T);
+      gs_st4<GS_NT_OUT>(out + pix, make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T));
     }
   }
   STAMP_SYNC();
@@ -1815,7 +1939,16 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if (!e2) w->sort_attr = true;
     return e2;
   };
-  const GsFused no_fu = {0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, nullptr};
+  // the blend's tile order (heaviest tiles of the previous frame first), built by the front end's
+  // first launch
+  uint32_t* order = nullptr;
+#if GS_TILE_ORDER
+  if (rows) {
+    if ((e = ensure(w->order, (size_t)tiles * 4))) return e;
+    order = (uint32_t*)w->order.p;
+  }
+#endif
+  const GsFused no_fu = {0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order};
 
   auto enqueue_fused = [&]() -> hipError_t {
     hipError_t e2;
@@ -1833,11 +1966,6 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     const uint32_t nwg = bgrid.bands * ((n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS);
     if ((e2 = ensure(w->fzp, (size_t)nwg * 8))) return e2;
     const uint32_t seq = ++w->seq;
-    uint32_t* order = nullptr;
-#if GS_TILE_ORDER
-    if ((e2 = ensure(w->order, (size_t)tiles * 4))) return e2;
-    if (rows) order = (uint32_t*)w->order.p;
-#endif
     GsFused fu = {scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
                   (uint32_t*)w->fzp.p, nwg, order};
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers
@@ -1925,9 +2053,10 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     hipError_t e2;
     if ((e2 = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e2;
     // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
-    hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks), dim3(GS_COUNT_THREADS), band_lds, s, cam, pa,
-                       bgrid, (uint32_t*)w->hist.p, (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev,
-                       (uint32_t*)w->nzbuf.p);
+    hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks + (order ? 1u : 0u)), dim3(GS_COUNT_THREADS),
+                       std::max(band_lds, (size_t)GS_ORDER_BUCKETS * 4), s, cam, pa, bgrid, (uint32_t*)w->hist.p,
+                       (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev, (uint32_t*)w->nzbuf.p,
+                       (const uint2*)w->ranges.p, order, cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x);
     if ((e2 = hipGetLastError())) return e2;
     if ((e2 = mark(1))) return e2;
     hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(GS_COLSCAN_THREADS), 0, s, bgrid, (uint32_t*)w->hist.p,

@@ -335,16 +335,20 @@ def _check_published(r, st, ref, out, n, what):
     assert err < 1e-4, (what, err)
 
 
-@pytest.mark.parametrize("n,W,H", [(100_000, 1920, 1080),  # C2
-                                   (20_000, 320, 180),     # tiles of 256-1000 pairs (in-blend and radix sorts)
-                                   (3000, 3840, 2160)])    # 4K: four bands of tile rows
-def test_gaussians_fused_front_end(native_lib, oracle_lib, n, W, H):
+@pytest.mark.parametrize("n,W,H,grow", [(100_000, 1920, 1080, 1.0),  # C2
+                                        (20_000, 320, 180, 1.0),     # tiles of 256-1000 pairs (in-blend and radix sorts)
+                                        (3000, 3840, 2160, 1.0),     # 4K: four bands of tile rows
+                                        (1500, 1920, 1080, 8.0)])    # chunks above 16 pairs per work-item: the re-walk
+def test_gaussians_fused_front_end(native_lib, oracle_lib, n, W, H, grow):
     """The single-launch front end (per-tile rows filled through atomic reservations) runs from the
     second frame of a context on (Gaussians in Morton order: the policy keeps it): its sorted keys /
     values / ranges, radii / tiles touched (bit-exact) and image (< 1e-4) equal the oracle's, as the
-    first (three-launch) frame's do."""
+    first (three-launch) frame's do. A chunk's pairs are kept in registers between its count and its
+    scatter up to GS_FUSED_QREG (16) per work-item; `grow` scales the Gaussians so that chunks exceed
+    that and walk their rects twice."""
     from pathtracer_gaussiansplatting_amd import Renderer
     g = Y.gaussians_c2(n, seed=9)
+    g["scales"] = g["scales"] * np.float32(grow)
     g["means"][1::53] = g["means"][0::53][: len(g["means"][1::53])]  # duplicated means: equal depths
     ubo = _gauss_ubo(W, H)
     ref = oracle_lib.splat_gaussians(g, ubo, W, H, bg=(0.1, 0.2, 0.3))

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Check 3DGS library variants against the base library on the C2 workload (and GS_N / GS_W / GS_H):
+"""Check 3DGS library variants against the base library on the C2 workload (and GS_N / GS_W / GS_H;
+GS_SORTED=2: the device Morton order with ids, so the published frame takes the fused front end):
 sorted keys / values / ranges bit-exact and the image identical (or its relative L2 printed).
 tools/gs_ab_check.py <variant> ...   (libptgs_<variant>.so next to libptgs.so)"""
 import os
@@ -15,8 +16,12 @@ def render(path, dg, ubo, W, H):
     from pathtracer_gaussiansplatting_amd import Renderer
     r = Renderer(0, lib_path=path, publish_splat_buffers=True)
     img = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
-    r.splat_gaussians(dg, ubo, W, H, img)  # a production frame first (no publish), then a published one
+    if os.environ.get("GS_SORTED", "0") == "2":  # device Morton order with ids (the fused front end's case)
+        dg = r.sort_gaussians_spatial(dg)
+    # a finished production frame first (no publish: it sizes the fused rows), then a published one
+    r.splat_gaussians(dg, ubo, W, H, img, want_stats=True)
     st = r.splat_gaussians(dg, ubo, W, H, img, want_stats=True)
+    print(f"  {os.path.basename(path)}: published frame {'fused' if st.fused else 'three launches'}", flush=True)
     torch.cuda.synchronize()
     b = r.splat_buffers()
     K = st.num_rendered
