@@ -787,7 +787,8 @@ __device__ __forceinline__ void gs_wg_walk(const uint32_t* s_incl, const uint4* 
 #ifndef GS_FUSED_KEEP
 #define GS_FUSED_KEEP 1
 #endif
-static_assert(GS_FUSED_THREADS <= 256 && GS_BAND_TILES <= 8192, "gs_wg_count_keep's packing");
+#define GS_KEEP_RB (GS_FUSED_THREADS <= 256 ? 8u : 9u)  // bits of rank and of j (< GS_FUSED_THREADS)
+static_assert(GS_FUSED_THREADS <= 512 && GS_BAND_TILES <= 8192, "gs_wg_count_keep's packing");
 __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, const uint4* s_e, uint32_t ng, uint32_t P,
                                                      uint32_t* s_hist, uint32_t bx0, uint32_t by0, uint32_t rw,
                                                      uint32_t (&pk)[GS_FUSED_QREG]) {
@@ -811,7 +812,7 @@ __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, con
     if (c < cnt) {
       const uint32_t k = ((e.y & 0xFFFFu) + ry - by0) * rw + ((e.x & 0xFFFFu) + rx - bx0);
       const uint32_t rank = atomicAdd(s_hist + k, 1u);
-      pk[c] = k | (rank << 13) | (j << 21);
+      pk[c] = k | (rank << 13) | (j << (13u + GS_KEEP_RB));
       if (c + 1 < cnt && ++rx == w) {
         rx = 0;
         if (++ry == (e.y >> 16)) {  // next rect with pairs
@@ -972,8 +973,8 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
 #pragma unroll
     for (uint32_t c = 0; c < GS_FUSED_QREG; ++c) {
       if (c < kept) {
-        const uint32_t k = pk[c] & 0x1FFFu, rel = s_hist[k] + ((pk[c] >> 13) & 0xFFu);
-        const uint4 e = s_e[pk[c] >> 21];
+        const uint32_t k = pk[c] & 0x1FFFu, rel = s_hist[k] + ((pk[c] >> 13) & ((1u << GS_KEEP_RB) - 1u));
+        const uint4 e = s_e[pk[c] >> (13u + GS_KEEP_RB)];
         uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13: exact after the fix-ups
         ry = ry * rw > k ? ry - 1 : ry;
         ry = (ry + 1) * rw <= k ? ry + 1 : ry;
