@@ -1299,7 +1299,43 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
 }
 
 // ---- blend ----------------------------------------------------------------------------------------
+// Merge ranking (tiles of more than GS_MERGE_MIN pairs): every wave sorts its 64 keys in registers
+// (bitonic network over the lanes, ascending), the sorted runs go to LDS, and a key's rank is its lane
+// plus, for every other run, the count of that run's keys below it (a binary search of 7 LDS reads):
+// ~200 VALU per key for 2-4 runs and ~400 for 8 instead of n / 4 compares against every key (the
+// counting below): keys are unique, so the ranks are the same.
+__device__ __forceinline__ unsigned long long gs_wave_sort64(unsigned long long x, uint32_t lane) {
+#pragma unroll
+  for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const unsigned long long y = __shfl_xor(x, (int)j);
+      const bool asc = (lane & k) == 0u, low = (lane & j) == 0u;
+      x = (asc == low) ? (y < x ? y : x) : (y < x ? x : y);
+    }
+  return x;
+}
+// keys of the sorted 64-key run b below x
+__device__ __forceinline__ uint32_t gs_run_below(const unsigned long long* b, unsigned long long x) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t step = 32; step; step >>= 1)
+    if (b[pos + step - 1] < x) pos += step;
+  return pos + (b[pos] < x ? 1u : 0u);
+}
+#ifndef GS_MERGE_MIN
+#define GS_MERGE_MIN 96u  // (counting is cheaper for up to ~1.5 runs)
+#endif
+#ifndef GS_RANK_MERGE
+#define GS_RANK_MERGE 1
+#endif
 #define GS_ARENA (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)  // staged records + per-quadrant lists
+#ifndef GS_RANK_SPLIT
+#define GS_RANK_SPLIT 0
+#endif
+#ifndef GS_RANK_PIPE
+#define GS_RANK_PIPE 0
+#endif
 #ifndef GS_SMALL_RANK
 // small tiles of at most this many pairs are ranked by counting instead of sorted by the register
 // bitonic network: blend 70.6 -> 68.1 us at C2 (kernel trace; 128: 67.8, within noise)
@@ -1357,6 +1393,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   unsigned long long* s_key = reinterpret_cast<unsigned long long*>(s_arena);
   __shared__ uint8_t s_mask[GS_BLOCK];
   __shared__ uint8_t s_sslot[GS_BLOCK];  // small tiles: staging slot of sorted position p
+#if GS_RANK_SPLIT
+  __shared__ uint16_t s_rpart[GS_BLOCK];  // small tiles: partial ranks of the split compares
+#endif
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   STAMP(1, 0);
   if (fu.scap) {
@@ -1481,12 +1520,88 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     // rank counting (keys are unique): every work-item of a wave holding keys counts the keys below
     // its own over all n in LDS (uniform reads, two keys per read, no barrier in the loop) and
     // records its staging slot at that rank
+#if GS_RANK_MERGE
+   if (n > GS_MERGE_MIN) {
+    // merge ranking: the wave's sorted run in LDS, ranks by binary searches of the other runs; the
+    // work-item holding a sorted key (its slot in the low 8 bits) records slot and published key
+    const uint32_t m = (n + 63u) >> 6;  // runs holding keys (uniform)
+    unsigned long long sk = ~0ull;
+    if (wave < m) {
+      sk = gs_wave_sort64(key, lane);
+      s_key[tid] = sk;
+    }
+    __syncthreads();
+    uint32_t r = lane;
+    if (wave < m) {
+      for (uint32_t q = 0; q < m; ++q)
+        if (q != wave) r += gs_run_below(s_key + 64u * q, sk);
+    }
+    __syncthreads();  // every read of the keys is done before records overwrite them
+    if (tid < n) s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
+    if (sk != ~0ull) {
+      if (keys_out) {
+        keys_out[range.x + r] = tbits | (sk >> 32);
+        vals_out[range.x + r] = (uint32_t)(sk >> 8) & 0xFFFFFFu;
+      }
+      s_sslot[r] = (uint8_t)(sk & 0xFFu);
+    }
+   } else
+#endif
+   {
+#if GS_RANK_SPLIT
+    // tiles of at most 128 pairs: the waves without keys take a share of the compares (the keys of
+    // the h waves holding them are counted against f = 4 / h ranges of j by f groups of h waves; the
+    // partial counts meet in LDS behind the barrier that ends the ranking anyway)
     s_key[tid] = key;  // ~0 above n
     __syncthreads();
     uint32_t r = 0;
+    const uint32_t hw = (n + 63u) >> 6;                       // waves holding keys (uniform)
+    const uint32_t f = hw == 1u ? 4u : hw == 2u ? 2u : 1u;    // groups sharing the compares
+    const uint32_t span = 64u * hw, part = f > 1u ? tid / span : 0u, ki = tid - part * span;
+    if (part < f && ki - lane < n) {
+      const unsigned long long kk = part ? s_key[ki] : key;
+      const uint32_t n8 = ((uint32_t)__builtin_amdgcn_readfirstlane((int)n) + 7u) & ~7u;
+      const uint32_t len = ((n8 / f) + 7u) & ~7u;
+      const uint32_t j0 = part * len, j1 = min(n8, j0 + len);
+      for (uint32_t j = j0; j < j1; j += 8) {
+        const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_key + j);
+        const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_key + j + 2);
+        const ulonglong2 x2 = *reinterpret_cast<const ulonglong2*>(s_key + j + 4);
+        const ulonglong2 x3 = *reinterpret_cast<const ulonglong2*>(s_key + j + 6);
+        r += ((uint32_t)(x0.x < kk) + (uint32_t)(x0.y < kk)) + ((uint32_t)(x1.x < kk) + (uint32_t)(x1.y < kk)) +
+             ((uint32_t)(x2.x < kk) + (uint32_t)(x2.y < kk)) + ((uint32_t)(x3.x < kk) + (uint32_t)(x3.y < kk));
+      }
+      if (part) s_rpart[tid] = (uint16_t)r;
+    }
+#else
+    s_key[tid] = key;  // ~0 above n
+    __syncthreads();
+    uint32_t r = 0;
+#ifdef GS_PROBE_NO_RANK  // (timing probe: identity ranks, wrong image)
+    r = tid;
+    if (false) {
+#else
     if (wave * 64u < n) {
+#endif
       // eight keys per step, four uniform reads in flight (entries n .. 255 hold ~0: never below a key)
       const uint32_t nu = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
+#if GS_RANK_PIPE
+      // the next eight keys' reads are issued before this eight's compares (entries up to 263 are read:
+      // the arena's records area, never compared for j >= n)
+      ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_key);
+      ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_key + 2);
+      ulonglong2 x2 = *reinterpret_cast<const ulonglong2*>(s_key + 4);
+      ulonglong2 x3 = *reinterpret_cast<const ulonglong2*>(s_key + 6);
+      for (uint32_t j = 0; j < nu; j += 8) {
+        const ulonglong2 y0 = *reinterpret_cast<const ulonglong2*>(s_key + j + 8);
+        const ulonglong2 y1 = *reinterpret_cast<const ulonglong2*>(s_key + j + 10);
+        const ulonglong2 y2 = *reinterpret_cast<const ulonglong2*>(s_key + j + 12);
+        const ulonglong2 y3 = *reinterpret_cast<const ulonglong2*>(s_key + j + 14);
+        r += ((uint32_t)(x0.x < key) + (uint32_t)(x0.y < key)) + ((uint32_t)(x1.x < key) + (uint32_t)(x1.y < key)) +
+             ((uint32_t)(x2.x < key) + (uint32_t)(x2.y < key)) + ((uint32_t)(x3.x < key) + (uint32_t)(x3.y < key));
+        x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+      }
+#else
       for (uint32_t j = 0; j < nu; j += 8) {
         const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_key + j);
         const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_key + j + 2);
@@ -1495,8 +1610,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         r += ((uint32_t)(x0.x < key) + (uint32_t)(x0.y < key)) + ((uint32_t)(x1.x < key) + (uint32_t)(x1.y < key)) +
              ((uint32_t)(x2.x < key) + (uint32_t)(x2.y < key)) + ((uint32_t)(x3.x < key) + (uint32_t)(x3.y < key));
       }
+#endif
     }
+#endif
     __syncthreads();  // every read of the keys is done before records overwrite them
+#if GS_RANK_SPLIT
+    if (part == 0)  // (the partial counts are in LDS)
+      for (uint32_t q = 1; q < f; ++q) r += s_rpart[tid + q * span];
+#endif
     if (tid < n) {
       s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
       if (keys_out) {
@@ -1505,6 +1626,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       }
       s_sslot[r] = (uint8_t)tid;
     }
+   }
    } else
 #endif
    {
@@ -1550,6 +1672,23 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       if (mid_lds) {
         // rank by counting (keys are unique: the gaussian is in the low word): each work-item ranks
         // its two keys against all n in LDS (uniform reads), then writes them to their ranks
+#if GS_RANK_MERGE
+        // merge ranking (above): wave w sorts runs w and w + 4 (slots tid and tid + 256)
+        unsigned long long k0 = tid < n ? seg[tid] : ~0ull;
+        unsigned long long k1 = tid + GS_BLOCK < n ? seg[tid + GS_BLOCK] : ~0ull;
+        const uint32_t m = (n + 63u) >> 6;  // runs holding keys: 5 .. 8 (uniform)
+        k0 = gs_wave_sort64(k0, lane);
+        if (wave + 4u < m) k1 = gs_wave_sort64(k1, lane);
+        s_key[tid] = k0;
+        s_key[tid + GS_BLOCK] = k1;
+        __syncthreads();
+        uint32_t r0 = lane, r1 = lane;
+        for (uint32_t q = 0; q < m; ++q) {
+          const unsigned long long* run = s_key + 64u * q;
+          if (q != wave) r0 += gs_run_below(run, k0);
+          if (q != wave + 4u && wave + 4u < m) r1 += gs_run_below(run, k1);
+        }
+#else
         const unsigned long long k0 = tid < n ? seg[tid] : ~0ull;
         const unsigned long long k1 = tid + GS_BLOCK < n ? seg[tid + GS_BLOCK] : ~0ull;
         s_key[tid] = k0;
@@ -1563,9 +1702,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
           r0 += ((x.x < k0) + (x.y < k0)) + ((y.x < k0) + (y.y < k0));
           r1 += ((x.x < k1) + (x.y < k1)) + ((y.x < k1) + (y.y < k1));
         }
+#endif
         __syncthreads();
-        if (tid < n) s_key[r0] = k0;
-        if (tid + GS_BLOCK < n) s_key[r1] = k1;
+        if (k0 != ~0ull) s_key[r0] = k0;  // (the slots below n hold exactly the keys other than ~0)
+        if (k1 != ~0ull) s_key[r1] = k1;
         __syncthreads();
         if (keys_out)
           for (uint32_t k = tid; k < n; k += GS_BLOCK) {
