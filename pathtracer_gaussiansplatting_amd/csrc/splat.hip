@@ -1330,12 +1330,6 @@ __device__ __forceinline__ uint32_t gs_run_below(const unsigned long long* b, un
 #define GS_RANK_MERGE 1
 #endif
 #define GS_ARENA (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)  // staged records + per-quadrant lists
-#ifndef GS_RANK_SPLIT
-#define GS_RANK_SPLIT 0
-#endif
-#ifndef GS_RANK_PIPE
-#define GS_RANK_PIPE 0
-#endif
 #ifndef GS_SMALL_RANK
 // small tiles of at most this many pairs are ranked by counting instead of sorted by the register
 // bitonic network: blend 70.6 -> 68.1 us at C2 (kernel trace; 128: 67.8, within noise)
@@ -1393,9 +1387,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   unsigned long long* s_key = reinterpret_cast<unsigned long long*>(s_arena);
   __shared__ uint8_t s_mask[GS_BLOCK];
   __shared__ uint8_t s_sslot[GS_BLOCK];  // small tiles: staging slot of sorted position p
-#if GS_RANK_SPLIT
-  __shared__ uint16_t s_rpart[GS_BLOCK];  // small tiles: partial ranks of the split compares
-#endif
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   STAMP(1, 0);
   if (fu.scap) {
@@ -1548,32 +1539,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
    } else
 #endif
    {
-#if GS_RANK_SPLIT
-    // tiles of at most 128 pairs: the waves without keys take a share of the compares (the keys of
-    // the h waves holding them are counted against f = 4 / h ranges of j by f groups of h waves; the
-    // partial counts meet in LDS behind the barrier that ends the ranking anyway)
-    s_key[tid] = key;  // ~0 above n
-    __syncthreads();
-    uint32_t r = 0;
-    const uint32_t hw = (n + 63u) >> 6;                       // waves holding keys (uniform)
-    const uint32_t f = hw == 1u ? 4u : hw == 2u ? 2u : 1u;    // groups sharing the compares
-    const uint32_t span = 64u * hw, part = f > 1u ? tid / span : 0u, ki = tid - part * span;
-    if (part < f && ki - lane < n) {
-      const unsigned long long kk = part ? s_key[ki] : key;
-      const uint32_t n8 = ((uint32_t)__builtin_amdgcn_readfirstlane((int)n) + 7u) & ~7u;
-      const uint32_t len = ((n8 / f) + 7u) & ~7u;
-      const uint32_t j0 = part * len, j1 = min(n8, j0 + len);
-      for (uint32_t j = j0; j < j1; j += 8) {
-        const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_key + j);
-        const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_key + j + 2);
-        const ulonglong2 x2 = *reinterpret_cast<const ulonglong2*>(s_key + j + 4);
-        const ulonglong2 x3 = *reinterpret_cast<const ulonglong2*>(s_key + j + 6);
-        r += ((uint32_t)(x0.x < kk) + (uint32_t)(x0.y < kk)) + ((uint32_t)(x1.x < kk) + (uint32_t)(x1.y < kk)) +
-             ((uint32_t)(x2.x < kk) + (uint32_t)(x2.y < kk)) + ((uint32_t)(x3.x < kk) + (uint32_t)(x3.y < kk));
-      }
-      if (part) s_rpart[tid] = (uint16_t)r;
-    }
-#else
     s_key[tid] = key;  // ~0 above n
     __syncthreads();
     uint32_t r = 0;
@@ -1585,23 +1550,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
 #endif
       // eight keys per step, four uniform reads in flight (entries n .. 255 hold ~0: never below a key)
       const uint32_t nu = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
-#if GS_RANK_PIPE
-      // the next eight keys' reads are issued before this eight's compares (entries up to 263 are read:
-      // the arena's records area, never compared for j >= n)
-      ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_key);
-      ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_key + 2);
-      ulonglong2 x2 = *reinterpret_cast<const ulonglong2*>(s_key + 4);
-      ulonglong2 x3 = *reinterpret_cast<const ulonglong2*>(s_key + 6);
-      for (uint32_t j = 0; j < nu; j += 8) {
-        const ulonglong2 y0 = *reinterpret_cast<const ulonglong2*>(s_key + j + 8);
-        const ulonglong2 y1 = *reinterpret_cast<const ulonglong2*>(s_key + j + 10);
-        const ulonglong2 y2 = *reinterpret_cast<const ulonglong2*>(s_key + j + 12);
-        const ulonglong2 y3 = *reinterpret_cast<const ulonglong2*>(s_key + j + 14);
-        r += ((uint32_t)(x0.x < key) + (uint32_t)(x0.y < key)) + ((uint32_t)(x1.x < key) + (uint32_t)(x1.y < key)) +
-             ((uint32_t)(x2.x < key) + (uint32_t)(x2.y < key)) + ((uint32_t)(x3.x < key) + (uint32_t)(x3.y < key));
-        x0 = y0; x1 = y1; x2 = y2; x3 = y3;
-      }
-#else
       for (uint32_t j = 0; j < nu; j += 8) {
         const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_key + j);
         const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_key + j + 2);
@@ -1610,14 +1558,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         r += ((uint32_t)(x0.x < key) + (uint32_t)(x0.y < key)) + ((uint32_t)(x1.x < key) + (uint32_t)(x1.y < key)) +
              ((uint32_t)(x2.x < key) + (uint32_t)(x2.y < key)) + ((uint32_t)(x3.x < key) + (uint32_t)(x3.y < key));
       }
-#endif
     }
-#endif
     __syncthreads();  // every read of the keys is done before records overwrite them
-#if GS_RANK_SPLIT
-    if (part == 0)  // (the partial counts are in LDS)
-      for (uint32_t q = 1; q < f; ++q) r += s_rpart[tid + q * span];
-#endif
     if (tid < n) {
       s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
       if (keys_out) {
