@@ -839,6 +839,7 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
                                                                          uint32_t order_tb, uint32_t order_te) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // <= band_rows * grid_x
   __shared__ uint32_t s_red[4][GS_FUSED_WG / 64];
+  __shared__ uint32_t s_tot[GS_FUSED_WG / 64];
   __shared__ uint32_t s_incl[GS_FUSED_THREADS];
   __shared__ uint4 s_e[GS_FUSED_THREADS];
   static_assert(GS_FUSED_THREADS >= GS_ORDER_BUCKETS, "gs_tile_order's buckets live in s_incl");
@@ -856,6 +857,10 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
   const uint32_t o = own && A.ids ? A.ids[i] : i;  // the key's index (the caller's)
   float d = 0.0f;  // view depth (every band's blocks need it for the keys; only band 0 stores it)
   if (own) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
+#ifdef GS_STAMP
+  if (threadIdx.x == 0) __builtin_amdgcn_s_waitcnt(0);  // (wave 0's preprocess, loads included)
+  STAMP(0, 6);
+#endif
   uint32_t xw, yh;
   gs_clip(rc, ty0, ty1, xw, yh);
   // the chunk's bounding tile rect (within the band): the LDS histogram covers only it, so zeroing
@@ -873,36 +878,35 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
     bx1 = max(bx1, (uint32_t)__shfl_xor((int)bx1, off));
     by1 = max(by1, (uint32_t)__shfl_xor((int)by1, off));
   }
+  // the rects and the inclusive scan of their areas for the workgroup walk: the per-wave partials of
+  // both (rect bounds, area totals) meet behind one barrier
+  const uint32_t area = yh ? (xw >> 16) * (yh >> 16) : 0u;
+  const uint32_t incl = wave_incl_scan(area);
   if (lane == 0) {
     s_red[0][wave] = bx0;
     s_red[1][wave] = by0;
     s_red[2][wave] = bx1;
     s_red[3][wave] = by1;
   }
+  if (lane == 63) s_tot[wave] = incl;
+  if (threadIdx.x < GS_FUSED_THREADS) s_e[threadIdx.x] = make_uint4(xw, yh, o, __float_as_uint(d));
   __syncthreads();
+  STAMP(0, 7);
+  uint32_t run = incl, P = 0;
 #pragma unroll
   for (uint32_t w = 0; w < GS_FUSED_WG / 64; ++w) {
     bx0 = min(bx0, s_red[0][w]);
     by0 = min(by0, s_red[1][w]);
     bx1 = max(bx1, s_red[2][w]);
     by1 = max(by1, s_red[3][w]);
+    const uint32_t tw = s_tot[w];
+    run += w < wave ? tw : 0u;
+    P += tw;
   }
+  if (threadIdx.x < GS_FUSED_THREADS) s_incl[threadIdx.x] = run;
   const uint32_t rw = bx1 > bx0 ? bx1 - bx0 : 0u, rh = by1 > by0 ? by1 - by0 : 0u, nt = rw * rh;
   for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_WG) s_hist[k] = 0;
-  // the rects and the inclusive scan of their areas for the workgroup walk
-  const uint32_t area = yh ? (xw >> 16) * (yh >> 16) : 0u;
-  const uint32_t incl = wave_incl_scan(area);
-  __syncthreads();  // (every wave has read s_red)
-  if (lane == 63) s_red[0][wave] = incl;
-  if (threadIdx.x < GS_FUSED_THREADS) s_e[threadIdx.x] = make_uint4(xw, yh, o, __float_as_uint(d));
-  __syncthreads();
-  {
-    uint32_t run = incl;
-    for (uint32_t w = 0; w < wave; ++w) run += s_red[0][w];
-    if (threadIdx.x < GS_FUSED_THREADS) s_incl[threadIdx.x] = run;
-  }
-  __syncthreads();
-  const uint32_t P = s_incl[GS_FUSED_THREADS - 1];
+  __syncthreads();  // (the scan and the zeroed histogram)
   STAMP(0, 1);
   STAMP_SYNC();
   STAMP(0, 2);

@@ -63,6 +63,10 @@ def main():
               f"last start {(f[:, 0].max() - f[:, 0].min()) * 0.01:.2f} us after the first")
         for k, nm in enumerate(["preprocess + rect + scan", "(sync)", "count walk", "reserve (atomics)", "scatter walk"]):
             stats(nm, f[:, k + 1] - f[:, k])
+        if f[:, 6].any():  # (wave 0's own preprocess; the rect's barrier; the scans)
+            stats("  preprocess (wave 0)", f[:, 6] - f[:, 0])
+            stats("  rect + barrier", f[:, 7] - f[:, 6])
+            stats("  zero + scan + 2 barriers", f[:, 1] - f[:, 7])
         stats("workgroup total", f[:, 5] - f[:, 0])
         print(f"  gap fused end -> first blend start {(b[:, 0].min() - f[:, 5].max()) * 0.01:.2f} us")
     print(f"blend: {len(b)} workgroups, span {(b[:, 3].max() - b[:, 0].min()) * 0.01:.2f} us, "
