@@ -52,6 +52,7 @@ struct ptgs_ctx {
   hipStream_t view_stream[PTGS_MAX_VIEWS] = {};
   hipEvent_t view_fork = nullptr, view_join[PTGS_MAX_VIEWS] = {};
   ptgs::WfWorkspace wf;  // wavefront path tracer buffers (PTGS_FLAG_PT_WAVEFRONT)
+  ptgs::PtSched pt_sched;  // megakernel tile schedule (heavy tiles first)
   void* comm = nullptr;  // RCCL communicator (ptgs_comm_create)
   int comm_ranks = 0, comm_rank = 0;
 };
@@ -158,6 +159,7 @@ void ptgs_destroy(ptgs_ctx* c) {
   free_scene(c);
   if (c->counters) (void)hipFree(c->counters);
   ptgs::wf_workspace_free(c->wf);
+  ptgs::free_pt_sched(c->pt_sched);
   splat_workspace_destroy(c->splat);
   for (int v = 0; v < PTGS_MAX_VIEWS; ++v) {
     if (c->view_ws[v]) splat_workspace_destroy(c->view_ws[v]);
@@ -496,7 +498,7 @@ int ptgs_trace_camera_rows(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_
     return PTGS_OK;
   }
   e = launch_pt_camera(c->dsc, cp, accum, w, h, row_begin, row_end, spp, ubo->frame_count, frame_stride, accum_mode,
-                       c->counters, stats, (hipStream_t)stream);
+                       c->counters, stats, &c->pt_sched, (hipStream_t)stream);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "pt_camera launch: %s", hipGetErrorString(e));
   return PTGS_OK;
 }

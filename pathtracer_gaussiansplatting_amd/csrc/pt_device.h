@@ -259,7 +259,7 @@ __device__ __forceinline__ void cswap4(Box4& b, int i, int j) {
   b.c[i] = sw ? cj : ci; b.c[j] = sw ? ci : cj;
 }
 
-template <bool STATS, bool TEX>
+template <bool STATS, bool TEX, int SS = PTGS_BLOCK>  // SS: the LDS stack's stride (work-items sharing it)
 __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
                                              TraversalCounters& cnt) {
   Hit h; h.t = r.tmax; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu; h.slot = 0;
@@ -272,8 +272,8 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   // candidate, so visiting order changes neither the hit nor the image.
   const int DONE = 0x7fffffff;
   int leaf = DONE;
-  auto push = [&](int x) { stack[(sp++) * PTGS_BLOCK] = x; };
-  auto pop = [&]() -> int { return sp ? stack[(--sp) * PTGS_BLOCK] : DONE; };
+  auto push = [&](int x) { stack[(sp++) * SS] = x; };
+  auto pop = [&]() -> int { return sp ? stack[(--sp) * SS] : DONE; };
   // (a register-cached stack top that hides the LDS read behind the node fetch measured -0.8%)
   for (;;) {
     while (node >= 0 && node != DONE) {
@@ -307,7 +307,7 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   }
 }
 
-template <bool STATS, bool TEX>
+template <bool STATS, bool TEX, int SS = PTGS_BLOCK>  // SS: the LDS stack's stride (work-items sharing it)
 __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
                                           TraversalCounters& cnt) {
   int sp = 0;
@@ -325,11 +325,11 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
       for (int j = 0; j < 4; ++j)
         if (b.tn[j] != __builtin_huge_valf()) {
           if (!have) { next = b.c[j]; have = true; }
-          else stack[(sp++) * PTGS_BLOCK] = b.c[j];
+          else stack[(sp++) * SS] = b.c[j];
         }
       if (!have) {
         if (sp == 0) return false;
-        node = stack[(--sp) * PTGS_BLOCK];
+        node = stack[(--sp) * SS];
         continue;
       }
       node = next;
@@ -350,7 +350,7 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
       return true;
     }
     if (sp == 0) return false;
-    node = stack[(--sp) * PTGS_BLOCK];
+    node = stack[(--sp) * SS];
   }
 }
 
@@ -533,13 +533,13 @@ __device__ __forceinline__ void shadow_towards(ShadowQuery& q, v3 o, v3 light_po
   q.tmax = dist - 0.005f;
 }
 
-template <bool STATS, bool TEX>
+template <bool STATS, bool TEX, int SS = PTGS_BLOCK>  // SS: the LDS stack's stride (work-items sharing it)
 __device__ __forceinline__ void resolve_shadow(ShadeCtx& c, v3& color, uint32_t seed, const ShadowQuery& q,
                                                TraversalCounters& cnt) {
   if (!(q.flags & SQ_TRACE)) return;
   c.shadow_rays++;
   const Ray r = make_ray(q.o, q.d, 0.001f, q.tmax);
-  float vis = trace_any<STATS, TEX>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
+  float vis = trace_any<STATS, TEX, SS>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
   vis = fmaxx(vis, q.trans);
   if (vis > 0.0f && (q.flags & SQ_VALID)) {
     v3 contrib = (q.pre * vis) * q.post;

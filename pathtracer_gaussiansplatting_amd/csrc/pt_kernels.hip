@@ -18,6 +18,15 @@
 #ifndef PTGS_PT_XCD_REMAP
 #define PTGS_PT_XCD_REMAP 0
 #endif
+#ifndef PTGS_PT_WG
+#define PTGS_PT_WG 64  // pt_camera_kernel workgroup: one wave per 8x8 pixel tile (256: four tiles per workgroup)
+#endif
+#ifndef PTGS_PT_SCHED
+#define PTGS_PT_SCHED 1  // heavy-tiles-first schedule of pt_camera_kernel (PtSched)
+#endif
+#ifndef PTGS_PT_SCHED_MIN
+#define PTGS_PT_SCHED_MIN (1u << 22)
+#endif
 
 namespace ptgs {
 
@@ -50,25 +59,53 @@ __device__ __forceinline__ void flush_counters(unsigned long long* counters, uin
 #define PTGS_PT_MIN_WAVES 4
 #endif
 
+// PT_STAMP builds (tools/pt_stamps.py): per-workgroup s_memrealtime (100 MHz) at start and end of
+// pt_camera_kernel, read back with ptgs_debug_pt_stamps (the schedule's tail)
+#ifdef PT_STAMP
+#define PT_STAMP_WG 65536  // (>= 32400 8x8 tiles at 1080p)
+__device__ unsigned long long g_pt_stamps[PT_STAMP_WG * 2];
+#endif
+
 template <bool STATS, bool TEX>
-__global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevScene sc, CamParams cp, float4* __restrict__ accum,
+__global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevScene sc, CamParams cp, float4* __restrict__ accum,
                                                         uint32_t W, uint32_t H, uint32_t row0, uint32_t row1,
                                                         uint32_t spp, uint32_t frame0, uint32_t stride,
-                                                        uint32_t mode, unsigned long long* counters) {
+                                                        uint32_t mode, unsigned long long* counters,
+                                                        const uint32_t* __restrict__ order, uint32_t* __restrict__ cost) {
   const uint32_t lid = threadIdx.x;
   const uint32_t wave = lid >> 6, lane = lid & 63u;
+#ifdef PT_STAMP
+  const uint32_t swg = blockIdx.y * gridDim.x + blockIdx.x;
+  if (lid == 0 && swg < PT_STAMP_WG) g_pt_stamps[2 * swg] = __builtin_amdgcn_s_memrealtime();
+#endif
 #if PTGS_PT_XCD_REMAP
+  static_assert(PTGS_PT_WG == 256, "the XCD remap maps 16x16 tiles");
   // XCD-aware: the workgroups of one XCD trace one horizontal strip of 16x16 tiles (shared L2 nodes)
   const uint32_t tl = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const uint32_t bx = tl % gridDim.x, by = tl / gridDim.x;
 #else
-  const uint32_t bx = blockIdx.x, by = blockIdx.y;
+  // tile schedule (PtSched): workgroup b renders tile order[b], the tiles that took longest in the
+  // previous launch first, so the launch ends on short tiles; each tile's time is recorded for the
+  // next launch. Any order gives the same image.
+  uint32_t bx = blockIdx.x, by = blockIdx.y;
+  if (order) {
+    const uint32_t tl = (uint32_t)__builtin_amdgcn_readfirstlane((int)order[blockIdx.y * gridDim.x + blockIdx.x]);
+    by = tl / gridDim.x;
+    bx = tl - by * gridDim.x;
+  }
+  const unsigned long long t_start = cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #endif
+#if PTGS_PT_WG == 64
+  // one wave per workgroup: its 8x8 tile; a finished tile frees its wave slot (and its LDS) at once
+  const uint32_t x = bx * 8u + (lane & 7u);
+  const uint32_t y = row0 + by * 8u + (lane >> 3);
+#else
   const uint32_t x = bx * 16u + (wave & 1u) * 8u + (lane & 7u);
   const uint32_t y = row0 + by * 16u + (wave >> 1) * 8u + (lane >> 3);
+#endif
   const bool active = (x < W) && (y < row1);
 
-  __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
+  __shared__ int s_stack[PTGS_STACK * PTGS_PT_WG];
   ShadeCtx c; c.sc = &sc; c.cp = &cp; c.stack = s_stack + threadIdx.x; c.shadow_rays = 0;
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
   uint32_t ext_rays = 0, samples = 0;
@@ -102,13 +139,13 @@ __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevSc
         p.depth = depth;
         Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
         ext_rays++;
-        Hit h = trace_closest<STATS, TEX>(sc, ray, p.seed, c.stack, tc);
+        Hit h = trace_closest<STATS, TEX, PTGS_PT_WG>(sc, ray, p.seed, c.stack, tc);
         if (STATS && h.gid != 0xffffffffu) tc.hits++;
         ShadowQuery q;
         q.flags = 0;
         if (h.gid == 0xffffffffu) miss<false>(cp, p);
         else closest_hit<false, TEX>(c, p, ray, h, q);
-        resolve_shadow<STATS, TEX>(c, p.color, p.seed, q, tc);  // NEE visibility after shading
+        resolve_shadow<STATS, TEX, PTGS_PT_WG>(c, p.color, p.seed, q, tc);  // NEE visibility after shading
         acc = acc + p.color * thr;
         acc = vmin(acc, 5.0f);
         if (p.hit_flag < 0.0f) break;
@@ -139,6 +176,16 @@ __global__ __launch_bounds__(256, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevSc
     else accum[pix] = make_float4(state.x, state.y, state.z, 1.0f);
   }
   flush_counters(counters, ext_rays, c.shadow_rays, samples, tc, STATS);
+#if !PTGS_PT_XCD_REMAP
+  if (cost) {
+    __syncthreads();  // (every wave of the tile is done)
+    if (lid == 0) cost[by * gridDim.x + bx] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - t_start, 0xFFFFFFFFull);
+  }
+#endif
+#ifdef PT_STAMP
+  __syncthreads();
+  if (lid == 0 && swg < PT_STAMP_WG) g_pt_stamps[2 * swg + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // Untextured: 4 waves per SIMD (the LDS stack's limit) — the single trace / shade site fits 128 VGPRs
@@ -276,20 +323,91 @@ __global__ __launch_bounds__(256) void pt_depth_kernel(DevScene sc, CamParams cp
   depth[(size_t)y * W + x] = d;
 }
 
+// One workgroup: the tiles by the previous launch's time, longest first (counting sort over 256
+// buckets of max / 256; the order inside a bucket is the LDS atomics')
+#define PT_ORDER_THREADS 1024
+__global__ __launch_bounds__(PT_ORDER_THREADS) void pt_order_kernel(const uint32_t* __restrict__ cost,
+                                                                    uint32_t* __restrict__ order, uint32_t n) {
+  __shared__ uint32_t s_h[256];
+  __shared__ uint32_t s_max[PT_ORDER_THREADS / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  uint32_t mx = 0;
+  for (uint32_t t = tid; t < n; t += PT_ORDER_THREADS) mx = max(mx, cost[t]);
+  for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+  if (lane == 0) s_max[tid >> 6] = mx;
+  if (tid < 256) s_h[tid] = 0;
+  __syncthreads();
+  mx = 0;
+  for (uint32_t w = 0; w < PT_ORDER_THREADS / 64; ++w) mx = max(mx, s_max[w]);
+  const float scale = 255.99f / (float)max(mx, 1u);
+  auto bucket = [&](uint32_t c) { return 255u - min(255u, (uint32_t)((float)c * scale)); };
+  for (uint32_t t = tid; t < n; t += PT_ORDER_THREADS) atomicAdd(s_h + bucket(cost[t]), 1u);
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the buckets, four per lane
+    const uint32_t c0 = s_h[4 * lane], c1 = s_h[4 * lane + 1], c2 = s_h[4 * lane + 2], c3 = s_h[4 * lane + 3];
+    const uint32_t sum = (c0 + c1) + (c2 + c3);
+    uint32_t incl = sum;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+      if (lane >= (uint32_t)off) incl += y;
+    }
+    const uint32_t ex = incl - sum;
+    s_h[4 * lane] = ex;
+    s_h[4 * lane + 1] = ex + c0;
+    s_h[4 * lane + 2] = ex + c0 + c1;
+    s_h[4 * lane + 3] = ex + c0 + c1 + c2;
+  }
+  __syncthreads();
+  for (uint32_t t = tid; t < n; t += PT_ORDER_THREADS) order[atomicAdd(s_h + bucket(cost[t]), 1u)] = t;
+}
+
+void free_pt_sched(PtSched& ps) {
+  if (ps.cost) (void)hipFree(ps.cost);
+  if (ps.order) (void)hipFree(ps.order);
+  ps = PtSched{};
+}
+
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
 hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accum, uint32_t W, uint32_t H,
                             uint32_t row0, uint32_t row1, uint32_t spp, uint32_t frame0, uint32_t stride,
-                            uint32_t mode, unsigned long long* counters, bool stats, hipStream_t stream) {
+                            uint32_t mode, unsigned long long* counters, bool stats, PtSched* ps,
+                            hipStream_t stream) {
   if (row1 <= row0 || spp == 0) return hipSuccess;
-  dim3 grid((W + 15u) / 16u, (row1 - row0 + 15u) / 16u);
-  dim3 block(256);
+  constexpr uint32_t T = PTGS_PT_WG == 64 ? 8u : 16u;  // tile edge
+  dim3 grid((W + T - 1u) / T, (row1 - row0 + T - 1u) / T);
+  dim3 block(PTGS_PT_WG);
+  const uint32_t *order = nullptr;
+  uint32_t* cost = nullptr;
+#if !PTGS_PT_XCD_REMAP
+  // heavy tiles first once a launch of this grid has recorded its tile times; launches of fewer than
+  // PTGS_PT_SCHED_MIN pixel-samples skip it (C1's 65k: the order kernel's launch would cost more than
+  // the tail it saves)
+  if (ps && PTGS_PT_SCHED && (uint64_t)W * (row1 - row0) * spp >= (uint64_t)PTGS_PT_SCHED_MIN) {
+    const uint32_t n = grid.x * grid.y;
+    hipError_t e;
+    if (n > ps->cap) {
+      free_pt_sched(*ps);
+      if ((e = hipMalloc(&ps->cost, (size_t)n * 4)) || (e = hipMalloc(&ps->order, (size_t)n * 4))) return e;
+      ps->cap = n;
+    }
+    if (ps->gx == grid.x && ps->gy == grid.y) {
+      hipLaunchKernelGGL(pt_order_kernel, dim3(1), dim3(PT_ORDER_THREADS), 0, stream, (const uint32_t*)ps->cost,
+                         ps->order, n);
+      if ((e = hipGetLastError())) return e;
+      order = ps->order;
+    }
+    ps->gx = grid.x;
+    ps->gy = grid.y;
+    cost = ps->cost;
+  }
+#endif
   // (STATS, TEX) instantiations: TEX only for scenes whose materials reference textures
   auto k = stats ? (sc.uses_textures ? pt_camera_kernel<true, true> : pt_camera_kernel<true, false>)
                  : (sc.uses_textures ? pt_camera_kernel<false, true> : pt_camera_kernel<false, false>);
   hipLaunchKernelGGL(k, grid, block, 0, stream, sc, cp, (float4*)accum, W, H, row0, row1, spp, frame0, stride, mode,
-                     counters);
+                     counters, order, cost);
   return hipGetLastError();
 }
 
@@ -314,3 +432,10 @@ hipError_t launch_pt_torus(const DevScene& sc, const CamParams& cp, const TorusP
 }
 
 }  // namespace ptgs
+
+#ifdef PT_STAMP
+extern "C" int ptgs_debug_pt_stamps(unsigned long long* host, unsigned int n) {
+  if (n > PT_STAMP_WG * 2u) n = PT_STAMP_WG * 2u;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ptgs::g_pt_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -19,9 +19,19 @@ struct ViewMat {  // ubo.view (column-major)
 hipError_t launch_pt_depth(const DevScene& sc, const CamParams& cp, const ViewMat& vm, float* depth, uint32_t W,
                            uint32_t H, uint32_t frame, hipStream_t stream);
 
+// The megakernel's tile schedule: per-tile times of the last launch and the order built from them
+// (tiles that took longest first); owned by the context, valid for the grid (gx, gy) it was recorded on
+struct PtSched {
+  uint32_t* cost = nullptr;
+  uint32_t* order = nullptr;
+  uint32_t cap = 0, gx = 0, gy = 0;
+};
+void free_pt_sched(PtSched& ps);
+
 hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accum, uint32_t W, uint32_t H,
                             uint32_t row0, uint32_t row1, uint32_t spp, uint32_t frame0, uint32_t stride,
-                            uint32_t mode, unsigned long long* counters, bool stats, hipStream_t stream);
+                            uint32_t mode, unsigned long long* counters, bool stats, PtSched* ps,
+                            hipStream_t stream);
 
 hipError_t launch_pt_torus(const DevScene& sc, const CamParams& cp, const TorusParams& tp,
                            const ptgs_ray_sample* samples, uint32_t n, uint32_t side, uint32_t frame,
