@@ -21,6 +21,9 @@
 #ifndef PTGS_PT_WG
 #define PTGS_PT_WG 64  // pt_camera_kernel workgroup: one wave per 8x8 pixel tile (256: four tiles per workgroup)
 #endif
+#ifndef PTGS_PT_PAIR
+#define PTGS_PT_PAIR 1  // one-wave workgroups: two lanes per pixel (even / odd samples) when spp >= 2
+#endif
 #ifndef PTGS_PT_SCHED
 #define PTGS_PT_SCHED 1  // heavy-tiles-first schedule of pt_camera_kernel (PtSched)
 #endif
@@ -96,10 +99,18 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
   const unsigned long long t_start = cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #endif
 #if PTGS_PT_WG == 64
-  // one wave per workgroup: its 8x8 tile; a finished tile frees its wave slot (and its LDS) at once
+  // One wave per workgroup. With spp >= 2 (pair) it shades an 8x4 tile with two lanes per pixel: lane
+  // l < 32 traces the even samples, l + 32 the odd ones, and after each pair the even lane folds both
+  // results into the pixel's running mean in sample order (the same operations, in the same order,
+  // as one lane tracing every sample): half the samples per lane, so a tile takes half as long and the
+  // launch's tail of last-started tiles is half as long. Otherwise an 8x8 tile, one sample stream.
+  const bool pair = PTGS_PT_PAIR && spp >= 2u;
+  const uint32_t half = pair ? lane >> 5 : 0u;
   const uint32_t x = bx * 8u + (lane & 7u);
-  const uint32_t y = row0 + by * 8u + (lane >> 3);
+  const uint32_t y = row0 + by * (pair ? 4u : 8u) + (pair ? (lane >> 3) & 3u : lane >> 3);
 #else
+  const bool pair = false;
+  const uint32_t half = 0;
   const uint32_t x = bx * 16u + (wave & 1u) * 8u + (lane & 7u);
   const uint32_t y = row0 + by * 16u + (wave >> 1) * 8u + (lane >> 3);
 #endif
@@ -110,23 +121,37 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
   uint32_t ext_rays = 0, samples = 0;
 
-  if (active) {
-    const size_t pix = (size_t)y * W + x;
-    v3 state = mk3(0.0f);
-    float state_a = 0.0f;
-    if (mode == PTGS_ACCUM_SUM || frame0 > 0) {
-      float4 prev = accum[pix];
-      state = mk3(prev.x, prev.y, prev.z);
-      state_a = prev.w;
+  const size_t pix = (size_t)y * W + x;
+  v3 state = mk3(0.0f);
+  float state_a = 0.0f;
+  if (active && half == 0u && (mode == PTGS_ACCUM_SUM || frame0 > 0)) {
+    float4 prev = accum[pix];
+    state = mk3(prev.x, prev.y, prev.z);
+    state_a = prev.w;
+  }
+  auto fold = [&](const v3& acc, uint32_t s) {  // raygen_camera.rgen:80-87, sample s
+    const uint32_t frame = frame0 + s * stride;
+    if (mode == PTGS_ACCUM_SUM) {
+      state = state + acc;
+      state_a = state_a + 1.0f;
+    } else if (frame > 0) {
+      float blend = 1.0f / (float)(frame + 1u);
+      state = mix3(state, acc, blend);
+    } else {
+      state = acc;
     }
-    for (uint32_t s = 0; s < spp; ++s) {
+  };
+  const uint32_t iters = pair ? (spp + 1u) >> 1 : spp;
+  for (uint32_t k = 0; k < iters; ++k) {
+    const uint32_t s = pair ? 2u * k + half : k;
+    v3 acc = mk3(0.0f);
+    if (active && s < spp) {
       const uint32_t frame = frame0 + s * stride;
       v3 ro, rd;
       float4 blue;
       uint32_t seed;
       primary_ray(sc, cp, x, y, W, H, frame, ro, rd, blue, seed);
 
-      v3 acc = mk3(0.0f);
       v3 thr = mk3(1.0f);
       Payload p;
       p.seed = seed;
@@ -161,17 +186,20 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
           thr = thr / pr;
         }
       }
-      if (mode == PTGS_ACCUM_SUM) {
-        state = state + acc;
-        state_a = state_a + 1.0f;
-      } else if (frame > 0) {
-        float blend = 1.0f / (float)(frame + 1u);
-        state = mix3(state, acc, blend);
-      } else {
-        state = acc;
-      }
       samples++;
     }
+    if (pair) {  // the odd sample's result from lane + 32 (every lane takes part in the exchange)
+      const v3 acc_odd = mk3(__shfl(acc.x, (int)(lane ^ 32u)), __shfl(acc.y, (int)(lane ^ 32u)),
+                             __shfl(acc.z, (int)(lane ^ 32u)));
+      if (active && half == 0u) {
+        fold(acc, s);
+        if (s + 1u < spp) fold(acc_odd, s + 1u);
+      }
+    } else if (active) {
+      fold(acc, s);
+    }
+  }
+  if (active && half == 0u) {
     if (mode == PTGS_ACCUM_SUM) accum[pix] = make_float4(state.x, state.y, state.z, state_a);
     else accum[pix] = make_float4(state.x, state.y, state.z, 1.0f);
   }
@@ -375,8 +403,10 @@ hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accu
                             uint32_t mode, unsigned long long* counters, bool stats, PtSched* ps,
                             hipStream_t stream) {
   if (row1 <= row0 || spp == 0) return hipSuccess;
-  constexpr uint32_t T = PTGS_PT_WG == 64 ? 8u : 16u;  // tile edge
-  dim3 grid((W + T - 1u) / T, (row1 - row0 + T - 1u) / T);
+  // tiles: 16x16 (256-thread workgroups), 8x8 (one wave), 8x4 (one wave, two lanes per pixel: spp >= 2)
+  const uint32_t tx = PTGS_PT_WG == 64 ? 8u : 16u;
+  const uint32_t ty = PTGS_PT_WG == 64 ? (PTGS_PT_PAIR && spp >= 2u ? 4u : 8u) : 16u;
+  dim3 grid((W + tx - 1u) / tx, (row1 - row0 + ty - 1u) / ty);
   dim3 block(PTGS_PT_WG);
   const uint32_t *order = nullptr;
   uint32_t* cost = nullptr;

@@ -32,7 +32,8 @@ def main():
     dll = C.CDLL(lib)
     dll.ptgs_debug_pt_stamps.argtypes = [C.c_void_p, C.c_uint]
     T = int(os.environ.get("PT_TILE", "8"))  # the workgroup tile edge (PTGS_PT_WG 64: 8, 256: 16)
-    nwg = ((W + T - 1) // T) * ((H + T - 1) // T)
+    TY = int(os.environ.get("PT_TILE_Y", "4" if T == 8 else str(T)))  # (8x4 tiles: two lanes per pixel)
+    nwg = ((W + T - 1) // T) * ((H + TY - 1) // TY)
     st = np.zeros(2 * nwg, np.uint64)
     assert dll.ptgs_debug_pt_stamps(st.ctypes.data, 2 * nwg) == 0
     st = st.reshape(-1, 2).astype(np.int64)
