@@ -24,6 +24,9 @@
 #ifndef PTGS_PT_PAIR
 #define PTGS_PT_PAIR 1  // one-wave workgroups: two lanes per pixel (even / odd samples) when spp >= 2
 #endif
+#ifndef PTGS_PT_LPP
+#define PTGS_PT_LPP 2  // most lanes per pixel (1, 2, 4)
+#endif
 #ifndef PTGS_PT_SCHED
 #define PTGS_PT_SCHED 1  // heavy-tiles-first schedule of pt_camera_kernel (PtSched)
 #endif
@@ -69,6 +72,13 @@ __device__ __forceinline__ void flush_counters(unsigned long long* counters, uin
 __device__ unsigned long long g_pt_stamps[PT_STAMP_WG * 2];
 #endif
 
+// lanes per pixel of the one-wave tiles (log2): up to PTGS_PT_LPP (1, 2 or 4) when there are that many
+// samples to share
+__host__ __device__ __forceinline__ uint32_t pt_lanes_log2(uint32_t spp) {
+  if (PTGS_PT_WG != 64 || !PTGS_PT_PAIR) return 0u;
+  return (PTGS_PT_LPP >= 4 && spp >= 4u) ? 2u : (PTGS_PT_LPP >= 2 && spp >= 2u) ? 1u : 0u;
+}
+
 template <bool STATS, bool TEX>
 __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevScene sc, CamParams cp, float4* __restrict__ accum,
                                                         uint32_t W, uint32_t H, uint32_t row0, uint32_t row1,
@@ -104,12 +114,16 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
   // results into the pixel's running mean in sample order (the same operations, in the same order,
   // as one lane tracing every sample): half the samples per lane, so a tile takes half as long and the
   // launch's tail of last-started tiles is half as long. Otherwise an 8x8 tile, one sample stream.
-  const bool pair = PTGS_PT_PAIR && spp >= 2u;
-  const uint32_t half = pair ? lane >> 5 : 0u;
-  const uint32_t x = bx * 8u + (lane & 7u);
-  const uint32_t y = row0 + by * (pair ? 4u : 8u) + (pair ? (lane >> 3) & 3u : lane >> 3);
+  const uint32_t llpp = pt_lanes_log2(spp);               // log2 lanes per pixel: 0, 1, 2 (uniform)
+  const bool pair = llpp != 0u;
+  const uint32_t lpp = 1u << llpp, pw = 64u >> llpp;       // lanes per pixel, pixels per wave
+  const uint32_t half = lane >> (6u - llpp);               // this lane's sample phase
+  const uint32_t pl = lane & (pw - 1u);                    // its pixel in the 8 x (8 / lpp) tile
+  const uint32_t x = bx * 8u + (pl & 7u);
+  const uint32_t y = row0 + by * (8u >> llpp) + (pl >> 3);
 #else
   const bool pair = false;
+  const uint32_t lpp = 1u, pw = 64u;
   const uint32_t half = 0;
   const uint32_t x = bx * 16u + (wave & 1u) * 8u + (lane & 7u);
   const uint32_t y = row0 + by * 16u + (wave >> 1) * 8u + (lane >> 3);
@@ -141,9 +155,9 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
       state = acc;
     }
   };
-  const uint32_t iters = pair ? (spp + 1u) >> 1 : spp;
+  const uint32_t iters = (spp + lpp - 1u) / lpp;
   for (uint32_t k = 0; k < iters; ++k) {
-    const uint32_t s = pair ? 2u * k + half : k;
+    const uint32_t s = k * lpp + half;
     v3 acc = mk3(0.0f);
     if (active && s < spp) {
       const uint32_t frame = frame0 + s * stride;
@@ -188,12 +202,19 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
       }
       samples++;
     }
-    if (pair) {  // the odd sample's result from lane + 32 (every lane takes part in the exchange)
-      const v3 acc_odd = mk3(__shfl(acc.x, (int)(lane ^ 32u)), __shfl(acc.y, (int)(lane ^ 32u)),
-                             __shfl(acc.z, (int)(lane ^ 32u)));
+    if (pair) {  // the other phases' results from lanes + pw, + 2 pw, + 3 pw (every lane exchanges)
+      v3 got[4];
+      got[0] = acc;
+#pragma unroll
+      for (uint32_t j = 1; j < 4; ++j) {
+        const int src = (int)((lane + j * pw) & 63u);
+        got[j] = mk3(__shfl(acc.x, src), __shfl(acc.y, src), __shfl(acc.z, src));
+        if (j + 1u >= lpp) break;
+      }
       if (active && half == 0u) {
-        fold(acc, s);
-        if (s + 1u < spp) fold(acc_odd, s + 1u);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+          if (j < lpp && s + j < spp) fold(got[j], s + j);
       }
     } else if (active) {
       fold(acc, s);
@@ -405,7 +426,7 @@ hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accu
   if (row1 <= row0 || spp == 0) return hipSuccess;
   // tiles: 16x16 (256-thread workgroups), 8x8 (one wave), 8x4 (one wave, two lanes per pixel: spp >= 2)
   const uint32_t tx = PTGS_PT_WG == 64 ? 8u : 16u;
-  const uint32_t ty = PTGS_PT_WG == 64 ? (PTGS_PT_PAIR && spp >= 2u ? 4u : 8u) : 16u;
+  const uint32_t ty = PTGS_PT_WG == 64 ? 8u >> pt_lanes_log2(spp) : 16u;
   dim3 grid((W + tx - 1u) / tx, (row1 - row0 + ty - 1u) / ty);
   dim3 block(PTGS_PT_WG);
   const uint32_t *order = nullptr;
