@@ -130,6 +130,25 @@ def test_sample_shard_sum_mode(pt, oracle_lib):
     assert np.all(g[..., 3] == 3.0)
 
 
+def test_tile_schedule_and_lane_pairs(pt, oracle_lib):
+    """Launches of >= 4M pixel-samples record each tile's time and the next launch of the same grid
+    renders the tiles longest first (PtSched); with spp >= 2 two lanes share a pixel (even / odd
+    samples, folded in sample order). The first launch (row-major order) and the second (heavy-first)
+    are bit-identical and equal the oracle, odd spp included (the last odd lane idles)."""
+    sc = U.cornell()
+    W = H = 512
+    spp = 17  # 512 * 512 * 17 = 4.46M pixel-samples: above PTGS_PT_SCHED_MIN
+    ubo = make_ubo(U.cornell_pose(), sc, 0)
+    g1, s1 = _gpu_render(pt, sc, ubo, W, H, spp)
+    g2, s2 = _gpu_render(pt, sc, ubo, W, H, spp)
+    assert np.array_equal(g1, g2)
+    assert (s1.extension_rays, s1.shadow_rays, s1.samples) == (s2.extension_rays, s2.shadow_rays, s2.samples)
+    o, so = _oracle_render(oracle_lib, sc, ubo, W, H, spp)
+    err, nd = _compare(g2, o, s2, so)
+    assert s2.samples == W * H * spp
+    print(f"scheduled cornell {W}x{H} {spp} spp: rel L2 {err:.2e}, {nd} pixels differ")
+
+
 def test_row_range(pt, oracle_lib):
     sc = U.cornell()
     ubo = make_ubo(U.cornell_pose(), sc, 0)
