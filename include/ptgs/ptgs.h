@@ -18,6 +18,10 @@
  *   - compute entry points are stream-ordered (hipStream_t passed as void*); the caller synchronises.
  *   - "device pointer" arguments must be device-accessible memory of the context's HIP device.
  *   - a context is not thread-safe (thread-compatible): one host thread at a time per context.
+ *   - a context owns device scratch its calls reuse (the splat workspace; the path tracer's tile
+ *     schedule: per-tile times of the last ptgs_trace_camera launch and the order built from them):
+ *     calls of one context on different streams must be ordered by the caller (events), or use one
+ *     context per stream (ptgs_splat_gaussians_views has its own per-view workspaces).
  */
 #ifndef PTGS_H_
 #define PTGS_H_
