@@ -99,6 +99,19 @@ def log2ceil(n):
     return max(0, math.ceil(math.log2(max(n, 1))))
 
 
+def gs_orbit_ubos(Camera, make_ubo, scene, W, H, frames):
+    """The viewer-protocol camera path of the gs_orbit leg: orbit the C2 cloud's centre (0, 0, -8) at
+    1.5 degrees per frame while dollying from 8 units (the C2 camera) to 5 and back."""
+    c = np.array([0.0, 0.0, -8.0])
+    out = []
+    for k in range(frames):
+        rr = 8.0 - 3.0 * math.sin(math.pi * k / max(1, frames - 1))
+        th = math.radians(1.5 * k)
+        eye = c + np.array([rr * math.sin(th), 0.1 * rr * math.sin(0.5 * th), rr * math.cos(th)])
+        out.append(make_ubo(Camera(aspect=W / H).look_at(eye.tolist(), c.tolist()), scene, 0))
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -140,14 +153,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def assert_complete(rr, where: str) -> int:
-        # every timed splat frame must have been rendered: the stream-ordered splat skips a frame whose
-        # pair count exceeds its buffer (ptgs_splat_status_read counts them); a skipped frame would make
-        # the timed loop cheaper than real work, so the bench refuses to report it
-        skipped = int(rr.splat_status(stream).frames)
-        if skipped:
-            raise SystemExit(f"bench: {skipped} splat frame(s) skipped in {where} (pair buffer too small)")
-        return skipped
+    def assert_complete(rr, where: str, strm=None) -> int:
+        # every timed splat frame must have been rendered completely: tiles that outgrow the buffers
+        # sized from earlier frames are completed through the spill pool on the device (counted); a
+        # frame whose spilled tiles exceed the pool would be incomplete (ptgs_splat_status_read counts
+        # those) and cheaper than real work, so the bench refuses to report it. Returns the spilled tiles.
+        st = rr.splat_status(stream if strm is None else strm)
+        if int(st.frames) or int(st.incomplete_tiles):
+            raise SystemExit(f"bench: {int(st.frames)} splat frame(s) incomplete in {where} (spill pool exhausted)")
+        return int(st.spilled_tiles)
 
     def sum_over_ranks(x: float) -> float:
         if world == 1:
@@ -366,7 +380,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         gdt = max_over_ranks(time.perf_counter() - t0)
-        assert_complete(r, "C2 timed loop")
+        c2_spilled = assert_complete(r, "C2 timed loop")
         # the same frames from the Gaussians in their generated (random) order: the same image bit for
         # bit, timed alone (secondary figure)
         img0 = torch.zeros_like(img)
@@ -403,7 +417,8 @@ def main():
         out["gs"] = {
             "value": round(N / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
             "workload": f"C2 3DGS forward: {N} synthetic Gaussians, {W}x{H}", "pairs_K": int(K),
-            "skipped_frames": 0,  # checked after every timed splat loop (ptgs_splat_status_read)
+            "skipped_frames": 0,  # incomplete frames: checked after every timed splat loop (ptgs_splat_status_read)
+            "spilled_tiles": c2_spilled,
             "scaling": "strong", "parallelism": "single GPU" if world == 1 else
             f"tile-row shard x{world} (rows balanced by pair counts: {gs_rows}) + row gather to rank 0"
             + (" (ptgs_gather_rows, RCCL)" if native_comm else " (gloo rehearsal, host copies)"),
@@ -434,34 +449,6 @@ def main():
             "note": "algorithmic: 8-B key + 48-B blend record per (Gaussian, tile) pair + 16 B per pixel"})
         out["gs"]["splat_pairs_per_s"] = round(K / (gdt / gsteps) / 1e9, 4)  # (Gaussian, tile) instances, G/s
         if world == 1:
-            # two frames in flight (the reference's MAX_FRAMES_IN_FLIGHT = 2): consecutive frames alternate
-            # between two contexts on two streams, so one frame's front end overlaps the other's blend
-            r2 = Renderer(dev)
-            s2 = torch.cuda.Stream()
-            img2 = torch.zeros_like(img)
-            pipes = [(r, stream, img), (r2, s2, img2)]
-            for k in range(4):
-                rk, sk, ik = pipes[k % 2]
-                rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
-            torch.cuda.synchronize()
-            r.splat_status(stream)
-            r2.splat_status(s2)
-            barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for k in range(gsteps):
-                rk, sk, ik = pipes[k % 2]
-                rk.splat_gaussians(dg, gubo, W, H, ik, stream=sk)
-            torch.cuda.synchronize()
-            barrier()
-            g2dt = max_over_ranks(time.perf_counter() - t0)
-            assert_complete(r, "two_in_flight")
-            assert_complete(r2, "two_in_flight (second context)")
-            out["gs"]["two_in_flight"] = {"value": round(N * world / (g2dt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
-                                          "ms_per_step": round(g2dt / gsteps * 1e3, 4),
-                                          "note": "same frames, alternating between two contexts / streams"}
-            r2.close()
-            del img2
             # four views of the C2 Gaussians per call (ptgs_splat_gaussians_views: forked streams, one
             # workspace per view), the capture-loop use: aggregate Gaussians x views per second
             vubos = [make_ubo(Camera(aspect=W / H).look_at([0.25 * k, 0.0, 0.0], [0.25 * k, 0.0, -1.0]),
@@ -482,6 +469,29 @@ def main():
                                    "ms_per_call": round(vdt * 1e3, 4),
                                    "note": "4 camera views of the C2 Gaussians per ptgs_splat_gaussians_views call"}
             del vouts
+            # the viewer's protocol (engine.cpp:2070-2072, camera.cpp:11): a new view every frame. The C2
+            # Gaussians under a camera orbiting the cloud's centre and dollying in and out; every frame
+            # stream-ordered (rows, pair buffer and tile order from the previous frame), timed in one run;
+            # tiles that outgrow the buffers are completed through the spill pool (counted)
+            orbit = gs_orbit_ubos(Camera, make_ubo, cornell_box_scene(), W, H, max(gsteps, 120))
+            for u in orbit[:3]:
+                r.splat_gaussians(dg, u, W, H, img, stream=stream)
+            torch.cuda.synchronize()
+            r.splat_status(stream)
+            t0 = time.perf_counter()
+            for u in orbit:
+                r.splat_gaussians(dg, u, W, H, img, stream=stream)
+            torch.cuda.synchronize()
+            odt = (time.perf_counter() - t0) / len(orbit)
+            o_spilled = assert_complete(r, "gs_orbit")
+            ks = []
+            for u in orbit[:: max(1, len(orbit) // 12)]:  # (untimed: the pair counts along the path)
+                ks.append(int(r.splat_gaussians(dg, u, W, H, img, want_stats=True, stream=stream).num_rendered))
+            out["gs"]["gs_orbit"] = {"value": round(N / odt / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(odt * 1e3, 4),
+                                     "frames": len(orbit), "skipped_frames": 0, "spilled_tiles": o_spilled,
+                                     "pairs_K_range": [min(ks), max(ks)],
+                                     "workload": f"C2 Gaussians, {len(orbit)} frames orbiting the cloud (1.5 deg per frame) "
+                                                 "while dollying from 8 to 5 units and back, stream-ordered"}
         del dg
         # the same forward at the C4 hybrid's Gaussian count (1M), splat only
         if world == 1 and not args.no_gs_1m:

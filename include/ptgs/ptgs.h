@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PTGS_ABI_VERSION 2
+#define PTGS_ABI_VERSION 3  /* 3: ptgs_gaussians.ids, ptgs_splat_stats.fused, ptgs_splat_status spill fields */
 
 /* ---------------- error codes ---------------- */
 #define PTGS_OK 0
@@ -42,6 +42,11 @@ extern "C" {
 #define PTGS_ENOSCENE (-3) /* trace before ptgs_scene_upload */
 #define PTGS_ERANGE (-4)   /* size exceeds an implementation limit */
 #define PTGS_EIO (-5)      /* file could not be read/parsed (host helpers) */
+#define PTGS_EINCOMPLETE (-6) /* an EARLIER stream-ordered splat frame of this context could not be completed
+                               * (its spill pool was exhausted: some tiles were left at the background).
+                               * Returned once, by the first splat call that starts after that frame has
+                               * finished on the device; that call has grown the pool and rendered its own
+                               * frame completely. ptgs_splat_reserve prevents it (see there). */
 
 /* ---------------- reference struct layouts (Appendix B of SURVEY.md) ---------------- */
 
@@ -339,7 +344,9 @@ typedef struct ptgs_gaussians {
     uint32_t count;
     /* NULL, or ids[i] = the caller's index of Gaussian i (u32 N, device): a reordered copy (e.g. from
      * ptgs_gaussians_sort_spatial) then renders exactly like the original order (sorted values, the
-     * depth tie rule and the per-Gaussian buffers use the ids) */
+     * depth tie rule and the per-Gaussian buffers use the ids). ids must be a permutation of [0, N):
+     * a Gaussian whose id is >= N is dropped (never written out of bounds) and the next splat call
+     * returns PTGS_EINVAL; duplicate ids are not detected (their keys collide: undefined order) */
     const uint32_t* ids;
 } ptgs_gaussians;
 
@@ -356,14 +363,20 @@ typedef struct ptgs_splat_stats {
  * [tile_row_begin, tile_row_end) are rendered (full frame: 0, ~0u) — screen-tile sharding of §8e;
  * pixels outside are left untouched.
  * Stream-ordered when stats == NULL: no host synchronisation, so a frame can be captured into and
- * replayed from a hipGraph. The (Gaussian, tile) pair buffer of the context's workspace starts at
- * 8 pairs per Gaussian (or ptgs_splat_reserve's size) and grows from the pair counts of earlier
- * frames. A frame whose pair count exceeds it is SKIPPED on the device (out is left untouched) and
- * counted: ptgs_splat_status reports every skipped frame, and the next call grows the buffer
- * (growth frees buffers, which waits for the device and invalidates graphs captured before it:
- * reserve, or capture after a frame with stats).
- * stats != NULL: the call waits for the frame's pair count, re-runs it after growing the buffer when
- * it did not fit (the frame is always complete and never counted as skipped) and fills stats. */
+ * replayed from a hipGraph. PTGS_OK means the frame is rendered completely, whatever the camera did
+ * since the previous frame: the (Gaussian, tile) pair buffer of the context's workspace (three-launch
+ * front end: 8 pairs per Gaussian or ptgs_splat_reserve's size, grown from the pair counts of earlier
+ * frames) and the per-tile rows of the fused front end (sized from an earlier frame's largest tile)
+ * are hints: a tile whose pairs did not fit them is gathered again and sorted by its own blend
+ * workgroup on the device, in the same launch, through a spill pool (max(2^20, N) pairs, grown from
+ * the demand of earlier frames) — same keys, same order, same image (ptgs_splat_status_read counts
+ * these spilled tiles). Only a frame whose spilled tiles exceed the spill pool is incomplete: those
+ * tiles are left at the background and the next call returns PTGS_EINCOMPLETE (see there);
+ * ptgs_splat_reserve(K) rules it out for frames of at most K pairs. Growth frees buffers, which
+ * waits for the device and invalidates graphs captured before it (reserve first).
+ * stats != NULL: the call waits for the earlier frames and for this frame's pair count; a frame with
+ * spilled tiles or above the pair buffer is re-run after growing the buffer (the exact published
+ * layout), and stats is filled. */
 int ptgs_splat_gaussians(ptgs_ctx* ctx, const ptgs_gaussians* g, const ptgs_ubo* ubo,
                          uint32_t width, uint32_t height, const float bg[3],
                          uint32_t tile_row_begin, uint32_t tile_row_end, float* out_rgba32f,
@@ -384,9 +397,8 @@ int ptgs_splat_gaussians_views(ptgs_ctx* ctx, const ptgs_gaussians* g, uint32_t 
  * run a single-launch front end: per-tile key rows of a fixed capacity (a power of two >= 1.25x that
  * tile, <= 2048 pairs) filled through per-tile atomic reservations, instead of the exact tile
  * segments of count + column scan + scatter (first frame, larger tiles, PTGS_GS_FRONTEND=three).
- * Both give the same keys, values, ranges and image. A frame with a tile above its row capacity is
- * skipped like an over-capacity frame (counted by ptgs_splat_status_read; with stats it is re-run
- * complete), and the next frame sizes its rows from it.
+ * Both give the same keys, values, ranges and image. A tile above its row capacity is completed
+ * through the spill pool (above), and the next frame sizes its rows from it.
  *
  * Spatial order: the fused front end reserves one run per (workgroup, touched tile); Gaussians whose
  * neighbours in memory are neighbours in space touch few tiles per workgroup. This writes a copy of
@@ -397,13 +409,15 @@ int ptgs_splat_gaussians_views(ptgs_ctx* ctx, const ptgs_gaussians* g, uint32_t 
 int ptgs_gaussians_sort_spatial(ptgs_ctx* ctx, const ptgs_gaussians* g, float* means, float* scales, float* rotations,
                                 float* opacities, float* colors, uint32_t* ids, void* hip_stream);
 
-/* Skipped-frame report of the stream-ordered splat (no stats): waits for hip_stream and the
- * context's view streams, then returns and clears the number of frames skipped since the last query
- * because their pair count exceeded the pair buffer. views[v]: frames of view slot v (slot 0 counts
- * ptgs_splat_gaussians / _over and view 0 of ptgs_splat_gaussians_views); frames = their sum.
- * pair_capacity: the smallest pair capacity over the slots in use; last_pairs: the largest pair count
- * any slot's latest frame produced. A frame reported here left its output untouched: render it
- * again (the buffers have grown by then), or call with stats. */
+/* Report of the stream-ordered splat (no stats): waits for hip_stream and the context's view streams,
+ * then returns (and clears) the counts since the last query. frames / views[v]: frames left
+ * incomplete (spill pool exhausted, see PTGS_EINCOMPLETE; each was also reported by a later call)
+ * per view slot v (slot 0 counts ptgs_splat_gaussians / _over and view 0 of
+ * ptgs_splat_gaussians_views); frames = their sum. spilled_tiles: tiles completed through the spill
+ * pool (rendered; a measure of how far the camera outran the buffers sized from earlier frames);
+ * incomplete_tiles: tiles left at the background. pair_capacity: the smallest pair capacity over the
+ * slots in use; last_pairs: the largest pair count any slot's latest frame produced; spill_capacity /
+ * spill_demand: slot 0's pool and the largest demand of one of its frames so far. */
 typedef struct ptgs_splat_status {
     uint64_t frames;
     uint32_t views[PTGS_MAX_VIEWS];
@@ -413,12 +427,19 @@ typedef struct ptgs_splat_status {
                              * reservations of the fused front end / nonzero histogram entries of the
                              * count: the spatial coherence of the Gaussians' order */
     uint32_t fused;         /* slot 0's latest frame ran the fused front end */
+    uint64_t spilled_tiles;
+    uint64_t incomplete_tiles;
+    uint32_t spill_capacity;
+    uint32_t spill_demand;
 } ptgs_splat_status;
 int ptgs_splat_status_read(ptgs_ctx* ctx, ptgs_splat_status* out, void* hip_stream);
 
-/* Grow the pair buffers of every view slot to at least `pairs` (Gaussian, tile) pairs so that
- * stream-ordered frames up to that count are never skipped (e.g. before capturing a hipGraph, or
- * from a previous frame's stats.num_rendered plus headroom). Synchronises the device when it grows. */
+/* Grow the pair buffers and spill pools of every view slot to at least `pairs` (Gaussian, tile) pairs:
+ * stream-ordered frames of up to that many pairs then store every pair (three-launch front end) or
+ * complete every spilled tile (fused rows: a frame's spilled tiles hold at most its pair count), so
+ * they are never incomplete — including hipGraph replays, whose row capacity is fixed at capture
+ * (e.g. before capturing, or from a previous frame's stats.num_rendered plus headroom).
+ * Synchronises the device when it grows. */
 int ptgs_splat_reserve(ptgs_ctx* ctx, uint32_t pairs);
 
 /* Hybrid composite (C4): the same splat, front to back over an image: a pixel stops at the first

@@ -10,12 +10,15 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptgs.so")
 
 PTGS_OK = 0
-ERRORS = {-1: "PTGS_EINVAL", -2: "PTGS_EHIP", -3: "PTGS_ENOSCENE", -4: "PTGS_ERANGE", -5: "PTGS_EIO"}
+ERRORS = {-1: "PTGS_EINVAL", -2: "PTGS_EHIP", -3: "PTGS_ENOSCENE", -4: "PTGS_ERANGE", -5: "PTGS_EIO",
+          -6: "PTGS_EINCOMPLETE"}
+PTGS_EINVAL = -1
+PTGS_EINCOMPLETE = -6
 ACCUM_RUNNING_MEAN = 0
 ACCUM_SUM = 1
 FLAG_COUNT_TRAVERSAL = 1
@@ -145,9 +148,12 @@ class SplatStats(C.Structure):
 
 
 class SplatStatus(C.Structure):
-    """ptgs_splat_status: frames the stream-ordered splat skipped (pair buffer too small)."""
+    """ptgs_splat_status: frames the stream-ordered splat left incomplete (spill pool exhausted), tiles
+    it completed through the spill pool, buffer capacities."""
     _fields_ = [("frames", C.c_uint64), ("views", C.c_uint32 * 8), ("pair_capacity", C.c_uint32),
-                ("last_pairs", C.c_uint32), ("touched_runs", C.c_uint32), ("fused", C.c_uint32)]
+                ("last_pairs", C.c_uint32), ("touched_runs", C.c_uint32), ("fused", C.c_uint32),
+                ("spilled_tiles", C.c_uint64), ("incomplete_tiles", C.c_uint64), ("spill_capacity", C.c_uint32),
+                ("spill_demand", C.c_uint32)]
 
 
 class SplatBuffers(C.Structure):
@@ -245,7 +251,9 @@ _lib = None
 
 
 class PtgsError(RuntimeError):
-    pass
+    def __init__(self, msg: str, code: int = 0):
+        super().__init__(msg)
+        self.code = code  # the PTGS_E* code (0: not from a library call)
 
 
 def load_library(path: str | None = None) -> C.CDLL:
@@ -276,7 +284,7 @@ def load_library(path: str | None = None) -> C.CDLL:
 
 def check(rc: int, what: str, err: str = "") -> None:
     if rc != PTGS_OK:
-        raise PtgsError(f"{what} failed: {ERRORS.get(rc, rc)} {err}")
+        raise PtgsError(f"{what} failed: {ERRORS.get(rc, rc)} {err}", rc)
 
 
 def fptr(a: np.ndarray):

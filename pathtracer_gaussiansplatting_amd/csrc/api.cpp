@@ -631,10 +631,15 @@ static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
   HIPCHK(c, hipSetDevice(c->device));
   float mvp[16];
   mat4_mul(ubo->proj, ubo->view, mvp);
+  uint32_t report = 0;
   hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, depth, under,
                                  tile_row_begin, tile_row_end, out, stats, (c->flags & PTGS_FLAG_TIME_STAGES) != 0,
-                                 (c->flags & PTGS_FLAG_SPLAT_PUBLISH) != 0, (hipStream_t)stream);
+                                 (c->flags & PTGS_FLAG_SPLAT_PUBLISH) != 0, (hipStream_t)stream, &report);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_gaussians: %s", hipGetErrorString(e));
+  // (this frame is rendered; the codes report an earlier frame of the workspace)
+  if (report & 2u) return fail(c, PTGS_EINVAL, "an earlier splat frame met ptgs_gaussians.ids entries >= count");
+  if (report & 1u)
+    return fail(c, PTGS_EINCOMPLETE, "an earlier splat frame left tiles incomplete (spill pool exhausted; grown)");
   return PTGS_OK;
 }
 
@@ -729,12 +734,18 @@ int ptgs_splat_status_read(ptgs_ctx* c, ptgs_splat_status* out, void* stream) {
   for (int v = 0; v < PTGS_MAX_VIEWS; ++v) {
     SplatWorkspace* ws = v == 0 ? c->splat : c->view_ws[v];
     if (!ws) continue;
-    uint32_t skipped = 0, cap = 0, last = 0;
-    splat_status(ws, true, &skipped, &cap, &last);
-    out->views[v] = skipped;
-    out->frames += skipped;
-    out->pair_capacity = std::min(out->pair_capacity, cap);
-    out->last_pairs = std::max(out->last_pairs, last);
+    SplatStatusOut so;
+    HIPCHK(c, splat_status(ws, true, &so));
+    out->views[v] = so.incomplete;
+    out->frames += so.incomplete;
+    out->spilled_tiles += so.spilled_tiles;
+    out->incomplete_tiles += so.incomplete_tiles;
+    out->pair_capacity = std::min(out->pair_capacity, so.capacity);
+    out->last_pairs = std::max(out->last_pairs, so.last_pairs);
+    if (v == 0) {
+      out->spill_capacity = so.spill_capacity;
+      out->spill_demand = so.spill_demand;
+    }
   }
   if (c->splat) splat_front_end_info(c->splat, &out->touched_runs, &out->fused);
   return PTGS_OK;

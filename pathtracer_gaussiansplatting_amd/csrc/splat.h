@@ -17,16 +17,25 @@ void splat_workspace_destroy(SplatWorkspace* w);
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
-                           ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s);
+                           ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s,
+                           uint32_t* report);  // report: bit 0 an earlier frame was left incomplete, bit 1 ids >= N
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
 // 3D Morton order of the means: a reordered copy + the original indices (synchronises s)
 hipError_t splat_sort_spatial(const ptgs_gaussians* g, float* means, float* scales, float* rots, float* opac,
                               float* colors, uint32_t* ids, hipStream_t s);
-// grow the pair buffers to at least `pairs` (frees / reallocates: waits for the device)
+// grow the pair buffers and the spill pool to at least `pairs` (frees / reallocates: waits for the device)
 hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs);
-// frames skipped on the device (pair count above the buffer) since the last clear; the pair
-// capacity; the latest pair count a frame published (call after the workspace's stream has drained)
-void splat_status(SplatWorkspace* w, bool clear, uint32_t* skipped, uint32_t* capacity, uint32_t* last_pairs);
+struct SplatStatusOut {
+  uint32_t incomplete;        // frames with a tile the spill pool could not hold (since the last clear)
+  uint32_t capacity;          // pair buffer
+  uint32_t last_pairs;        // the latest pair count a frame published
+  uint32_t spilled_tiles;     // tiles completed through the spill pool (since the last clear)
+  uint32_t incomplete_tiles;  // tiles left at the background (pool exhausted; since the last clear)
+  uint32_t spill_capacity;    // spill pool (pairs)
+  uint32_t spill_demand;      // the largest spill demand of a frame so far (pairs)
+};
+// call after the workspace's stream has drained (reads device counters)
+hipError_t splat_status(SplatWorkspace* w, bool clear, SplatStatusOut* out);
 // the latest pair count any frame of this workspace published (a hint: no wait)
 uint32_t splat_pair_hint(const SplatWorkspace* w);
 // the latest frame's touched (workgroup, tile) runs and whether it ran the fused front end

@@ -57,9 +57,13 @@ struct DevBuf {
 struct SplatWorkspace {
   DevBuf means2d, depths, conic, rec, radii, touched, pairs, keys_out, vals_out, ranges, hist, tile_info,
       group_total, tile_slots, point_keys, total, rect, large, large_ctr, sort_scratch;
-  DevBuf cursor, fz, pub_offs, keys_pub, vals_pub;  // fused front end (see gs_bin_fused_kernel)
+  DevBuf cursor, fz, pub_offs, keys_pub, vals_pub;  // fused front end (see gs_bin_fused_kernel); fz: counters
   DevBuf dbg_depths, fzp, nzbuf, order;  // order: the blend's tile order (heavy first, fused frames)
-  uint32_t seq = 0;           // fused frames enqueued (the overflow word's tag)
+  DevBuf crect, sp_keys, sp_vals;  // spilled tiles (gs_spill_tile): chunk rects, the spill pool
+  uint32_t sp_cap = 0;        // spill pool capacity (pairs)
+  uint32_t incomplete = 0;    // frames reported incomplete (spill pool exhausted) since the last status clear
+  uint32_t spilled_base = 0, incomplete_base = 0;  // device counters fz[9] / fz[10] at the last status clear
+  bool ids_error = false;     // a frame met an out-of-range ptgs_gaussians.ids entry
   bool have_hint = false;     // a finished frame has published its largest tile: the fused path can size its rows
   bool hint_recorded = false;
   hipEvent_t hint_event = nullptr;
@@ -84,7 +88,8 @@ void splat_workspace_destroy(SplatWorkspace* w) {
   DevBuf* all[] = {&w->means2d, &w->depths, &w->conic, &w->rec, &w->radii, &w->touched, &w->pairs, &w->keys_out,
                    &w->vals_out, &w->ranges, &w->hist, &w->tile_info, &w->group_total, &w->tile_slots, &w->point_keys,
                    &w->total, &w->rect, &w->large, &w->large_ctr, &w->sort_scratch, &w->cursor, &w->fz,
-                   &w->pub_offs, &w->keys_pub, &w->vals_pub, &w->dbg_depths, &w->fzp, &w->nzbuf};
+                   &w->pub_offs, &w->keys_pub, &w->vals_pub, &w->dbg_depths, &w->fzp, &w->nzbuf, &w->order,
+                   &w->crect, &w->sp_keys, &w->sp_vals};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
@@ -127,6 +132,7 @@ struct PreArgs {
   float4* rec;
   const uint32_t* ids;  // caller's index of Gaussian i (NULL: i): keys, values, records and the
                         // per-Gaussian outputs use it, so a reordered set renders like the original
+  uint32_t* bad_ids;    // pinned host word set to 1 when an id is >= n (the Gaussian is dropped)
 };
 
 // Stores that may stream past L2 (A/B: GS_NT_REC for the blend records, GS_NT_OUT for the image)
@@ -169,12 +175,14 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   // walk, at i) and radii / touched / means2d / conic (ptgs_splat_get_buffers) when their pointers are
   // set (the fused path without PTGS_FLAG_SPLAT_PUBLISH leaves them out)
   const uint32_t o = A.ids ? A.ids[i] : i;
-  if (STORE) {
-    if (radii) {
-      radii[o] = 0;
-      touched[o] = 0;
-    }
-    if (rects) rects[i] = none;  // empty rect: the scatter reads rects only
+  if (STORE && rects) rects[i] = none;  // empty rect: the scatter reads rects only
+  if (o >= A.n) {  // ids must be a permutation of [0, n): an index outside it is dropped, not written
+    if (STORE) __atomic_store_n(A.bad_ids, 1u, __ATOMIC_RELAXED);  // (reported by the next call)
+    return none;
+  }
+  if (STORE && radii) {
+    radii[o] = 0;
+    touched[o] = 0;
   }
   float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   // every input is loaded here, before the depth test: one memory round trip per Gaussian (loads
@@ -464,6 +472,50 @@ __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restri
   for (uint32_t t = tb + tid; t < te; t += nth) order[atomicAdd(s_h + gs_order_bucket(prev[t]), 1u)] = t;
 }
 
+// Spill accounting (see gs_spill_tile), run by the first front-end launch's block (0, 0): the previous
+// frame's spill demand (fz[8], the pool cursor its spilled tiles advanced; that frame's blend has
+// finished: stream order) goes to the host (k_host[8], the pool's next size) and the running maximum
+// (fz[11]); the cursor restarts at 0 for this frame's blend.
+__device__ __forceinline__ void gs_spill_rearm(uint32_t* fz, uint32_t* k_host) {
+  const uint32_t d = fz[8];
+  __atomic_store_n(k_host + 8, d, __ATOMIC_RELAXED);
+  if (d > fz[11]) fz[11] = d;
+  fz[8] = 0;
+  __threadfence_system();
+}
+
+// Bounding tile rect (x0, y0, x1, y1) of one front-end workgroup's clipped Gaussian rects, reduced over
+// the workgroup (every work-item passes its running bounds; s_r: 4 x waves words of LDS); work-item 0
+// stores it (empty: x0 > x1). A spilled tile's blend workgroup looks only at the chunks whose rect
+// holds it.
+template <uint32_t NT>
+__device__ __forceinline__ void gs_store_chunk_rect(uint32_t bx0, uint32_t by0, uint32_t bx1, uint32_t by1,
+                                                    uint32_t (*s_r)[NT / 64], ushort4* crect, uint32_t wg) {
+  for (int off = 32; off > 0; off >>= 1) {
+    bx0 = min(bx0, (uint32_t)__shfl_xor((int)bx0, off));
+    by0 = min(by0, (uint32_t)__shfl_xor((int)by0, off));
+    bx1 = max(bx1, (uint32_t)__shfl_xor((int)bx1, off));
+    by1 = max(by1, (uint32_t)__shfl_xor((int)by1, off));
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    s_r[0][threadIdx.x >> 6] = bx0;
+    s_r[1][threadIdx.x >> 6] = by0;
+    s_r[2][threadIdx.x >> 6] = bx1;
+    s_r[3][threadIdx.x >> 6] = by1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < NT / 64; ++w) {
+      bx0 = min(bx0, s_r[0][w]);
+      by0 = min(by0, s_r[1][w]);
+      bx1 = max(bx1, s_r[2][w]);
+      by1 = max(by1, s_r[3][w]);
+    }
+    crect[wg] = bx0 < bx1 ? make_ushort4((unsigned short)bx0, (unsigned short)by0, (unsigned short)bx1, (unsigned short)by1)
+                          : make_ushort4(1, 1, 0, 0);
+  }
+}
+
 // preprocess + count. Block (0, 0) also re-arms the frame's counters.
 __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                       uint32_t* __restrict__ hist,
@@ -472,7 +524,8 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
                                                                       uint32_t* k_host, uint32_t* __restrict__ nzbuf,
                                                                       const uint2* __restrict__ prev_ranges,
                                                                       uint32_t* __restrict__ order, uint32_t order_tb,
-                                                                      uint32_t order_te) {
+                                                                      uint32_t order_te, uint32_t* __restrict__ fz,
+                                                                      ushort4* __restrict__ crect) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // band_rows * grid_x (>= GS_ORDER_BUCKETS)
   if (order && blockIdx.y == gridDim.y - 1) {  // the extra row of blocks: the blend's tile order
     if (blockIdx.x == 0) gs_tile_order(prev_ranges, order, order_tb, order_te, s_hist);
@@ -485,17 +538,25 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     total[1] = 0;  // largest tile (colscan's atomicMax; the scatter hands it to the host)
     large_ctr[0] = 0;  // large-tile list length (colscan)
+    gs_spill_rearm(fz, k_host);
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t b0 = blockIdx.y * bg.chunk, b1 = min(A.n, b0 + bg.chunk);
+  uint32_t bx0 = 0xFFFFu, by0 = 0xFFFFu, bx1 = 0u, by1 = 0u;  // the chunk's rect in the band (gs_spill_tile)
   for (uint32_t base = b0 + wave * 64u; base < b1; base += GS_COUNT_THREADS) {
     const uint32_t i = base + lane;
     ushort4 rc = make_ushort4(0, 0, 0, 0);
     if (i < b1) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i) : gs_preprocess_one<false>(cam, A, i);
-#ifndef GS_PROBE_NO_WALK
     uint32_t xw, yh;
     gs_clip(rc, ty0, ty1, xw, yh);
+    if (yh) {
+      bx0 = min(bx0, xw & 0xFFFFu);
+      bx1 = max(bx1, (xw & 0xFFFFu) + (xw >> 16));
+      by0 = min(by0, yh & 0xFFFFu);
+      by1 = max(by1, (yh & 0xFFFFu) + (yh >> 16));
+    }
+#ifndef GS_PROBE_NO_WALK
     if (__ballot(yh != 0u))
       gs_expand<false>(lane, i, xw, yh, 0.0f, [&](uint32_t, uint32_t x, uint32_t y, float) {
         atomicAdd(s_hist + (y - ty0) * bg.grid_x + x, 1u);
@@ -522,6 +583,8 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
     for (uint32_t w = 0; w < GS_COUNT_THREADS / 64; ++w) t += s_nz[w];
     nzbuf[blockIdx.y * gridDim.x + blockIdx.x] = t;  // (summed by the scatter's block (0, 0): no fan-in atomics)
   }
+  __shared__ uint32_t s_rr[4][GS_COUNT_THREADS / 64];
+  gs_store_chunk_rect<GS_COUNT_THREADS>(bx0, by0, bx1, by1, s_rr, crect, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
 // One 256-work-item block per 64-tile group g: wave w sums chunks [w*cpw, (w+1)*cpw) of the group's
@@ -641,12 +704,10 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     __atomic_store_n(k_host + 5, 0u, __ATOMIC_RELAXED);
     __atomic_store_n(k_host + 6, 2u, __ATOMIC_RELAXED);  // published by: three launches
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
-    // a frame that does not fit is skipped by this kernel, the sort and the blend: count it for
-    // ptgs_splat_status_read (one writer per workspace: its frames are ordered on one stream)
-    if (carry > cap) __atomic_store_n(k_host + 3, __atomic_load_n(k_host + 3, __ATOMIC_RELAXED) + 1u, __ATOMIC_RELAXED);
     __threadfence_system();  // visible to the host before the kernel ends (the K event has no system fence)
   }
-  if (carry > cap) return;
+  // (K above the pair buffer: the tiles whose segment ends beyond it keep none of their pairs here and
+  // are rendered by the blend through gs_spill_tile; the fixed rows of small tiles always fit)
   for (uint32_t k = tid; k < nt; k += GS_BIN_THREADS) {
     const uint32_t t = t0 + k;
     const uint2 ti = tile_info[t];
@@ -665,10 +726,12 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     const unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | i;
     const uint32_t k = (y - ty0) * bg.grid_x + x;
     const uint32_t rel = atomicAdd(s_cur + k, 1u), dst = s_tot[k];
-    if (dst & 0x80000000u)
-      pairs[(dst & 0x7FFFFFFFu) + rel] = key;
-    else
+    if (dst & 0x80000000u) {
+      const uint32_t at = (dst & 0x7FFFFFFFu) + rel;
+      if (at < cap) pairs[at] = key;
+    } else {
       tile_slots[dst + rel] = key;
+    }
   };
 #if GS_SCATTER_DIRECT
   if (bg.bands == 1) {  // one band: every rect meets it, so no filtering ring (one Gaussian per lane, as the count)
@@ -700,15 +763,16 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
 // tile_slots[t * scap + base + LDS rank]. The order inside a row depends on the atomics' order and is
 // fixed by the per-tile sort (keys are unique), so keys / values / image equal the three-launch path.
 // The blend reads the tile's count from its cursor and zeroes it (cursors are zero between frames).
-// A tile whose count exceeds scap marks the frame (fz[2] = seq): sort and blend skip it, the host
-// counts it and falls back to the three-launch path. fz: [1] largest tile above 256, [2] overflow
-// sequence, [4] tiles above GS_MID pairs; per workgroup fzp: (pairs, reservations); published to the
-// host by the blend's block (0, 0).
+// A tile whose count exceeds scap keeps its first scap keys only: the blend renders it through
+// gs_spill_tile (its pairs gathered again from the per-Gaussian rects / depths band 0 stores here and
+// the per-workgroup chunk rects), so the frame is complete; the next frame sizes its rows from it.
+// fz: [1] largest tile above 256, [4] tiles above GS_MID pairs, [5] tiles above scap; per workgroup
+// fzp: (pairs, reservations); published to the host by the blend's block (0, 0).
 #ifndef GS_FUSED_THREADS
 #define GS_FUSED_THREADS 256  // Gaussians per fused workgroup (512 / 1 024 work-items: 1.5 us slower at C2)
 #endif
 struct GsFused {  // the sort's and the blend's view of a fused-front-end frame (scap == 0: three-launch path)
-  uint32_t scap, seq;
+  uint32_t scap;
   uint32_t* cursor;   // per-tile pair counts (zeroed again by the blend)
   uint32_t* fz;       // counters (see above)
   uint32_t* k_host;   // pinned host words (published by blend block (0, 0))
@@ -829,14 +893,18 @@ __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, con
 }
 
 __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
-                                                                         uint32_t scap, uint32_t seq,
+                                                                         uint32_t scap,
                                                                          uint32_t* __restrict__ cursor,
                                                                          uint32_t* __restrict__ fz,
                                                                          uint32_t* __restrict__ fzp,
                                                                          unsigned long long* __restrict__ tile_slots,
                                                                          const uint2* __restrict__ prev_ranges,
                                                                          uint32_t* __restrict__ order,
-                                                                         uint32_t order_tb, uint32_t order_te) {
+                                                                         uint32_t order_tb, uint32_t order_te,
+                                                                         ushort4* __restrict__ crect,
+                                                                         ushort4* __restrict__ rects_out,
+                                                                         float* __restrict__ depths_out,
+                                                                         uint32_t* k_host) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // <= band_rows * grid_x
   __shared__ uint32_t s_red[4][GS_FUSED_WG / 64];
   __shared__ uint32_t s_tot[GS_FUSED_WG / 64];
@@ -857,6 +925,11 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
   const uint32_t o = own && A.ids ? A.ids[i] : i;  // the key's index (the caller's)
   float d = 0.0f;  // view depth (every band's blocks need it for the keys; only band 0 stores it)
   if (own) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
+  if (own && blockIdx.x == 0) {  // for gs_spill_tile: the rect (empty: culled) and depth in walk order
+    rects_out[i] = rc;
+    depths_out[i] = d;
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) gs_spill_rearm(fz, k_host);
 #ifdef GS_STAMP
   if (threadIdx.x == 0) __builtin_amdgcn_s_waitcnt(0);  // (wave 0's preprocess, loads included)
   STAMP(0, 6);
@@ -905,6 +978,10 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
   }
   if (threadIdx.x < GS_FUSED_THREADS) s_incl[threadIdx.x] = run;
   const uint32_t rw = bx1 > bx0 ? bx1 - bx0 : 0u, rh = by1 > by0 ? by1 - by0 : 0u, nt = rw * rh;
+  if (threadIdx.x == 0)  // the workgroup's bounding rect (gs_spill_tile; empty: x0 > x1)
+    crect[blockIdx.y * gridDim.x + blockIdx.x] =
+        nt ? make_ushort4((unsigned short)bx0, (unsigned short)by0, (unsigned short)bx1, (unsigned short)by1)
+           : make_ushort4(1, 1, 0, 0);
   for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_WG) s_hist[k] = 0;
   __syncthreads();  // (the scan and the zeroed histogram)
   STAMP(0, 1);
@@ -946,7 +1023,7 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
       s_hist[k0 + j * GS_FUSED_WG] = base[j];
       pairs += c[j];
       ++res;
-      if (base[j] + c[j] > scap) __hip_atomic_store(fz + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (base[j] <= scap && base[j] + c[j] > scap) atomicAdd(fz + 5, 1u);  // (one crossing per spilled tile)
       if (base[j] + c[j] > 256u) {
         atomicMax(fz + 1, base[j] + c[j]);
         if (base[j] <= GS_MID && base[j] + c[j] > GS_MID) atomicAdd(fz + 4, 1u);  // (one crossing per tile)
@@ -1252,16 +1329,18 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
   uint32_t count;
   if (fu.scap) {
     // fused front end: no tile list; block b checks tiles b, b + grid, ... (<= 256 of them: the host
-    // sizes the grid) by their cursors and sorts those above GS_MID pairs
-    if (__hip_atomic_load(fu.fz + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fu.seq) return;
+    // sizes the grid) by their cursors and sorts those above GS_MID pairs that fit their rows (a
+    // spilled tile, above scap, is gathered and sorted by its blend workgroup: gs_spill_tile)
     if (tid == 0) s_list[GS_SORT_THREADS] = 0;
     __syncthreads();
     const uint32_t t = blockIdx.x + tid * gridDim.x;
-    if (t < ntiles && fu.cursor[t] > GS_MID) s_list[atomicAdd(&s_list[GS_SORT_THREADS], 1u)] = t;
+    if (t < ntiles) {
+      const uint32_t c = fu.cursor[t];
+      if (c > GS_MID && c <= fu.scap) s_list[atomicAdd(&s_list[GS_SORT_THREADS], 1u)] = t;
+    }
     __syncthreads();
     count = s_list[GS_SORT_THREADS];
   } else {
-    if (*total > cap) return;
     count = large_ctr[0];
   }
   // static striding over the list (a shared work counter serialises: ~30 ns per contended atomic,
@@ -1269,6 +1348,7 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
   for (uint32_t li = fu.scap ? 0 : blockIdx.x; li < count; li += fu.scap ? 1 : gridDim.x) {
     const uint32_t tile = fu.scap ? s_list[li] : large[li];
     const uint2 range = fu.scap ? make_uint2(tile * fu.scap, tile * fu.scap + fu.cursor[tile]) : ranges[tile];
+    if (!fu.scap && range.y > cap) continue;  // segment beyond the pair buffer: spilled (gs_spill_tile)
     const uint32_t n = range.y - range.x;
     unsigned long long* seg = fu.scap ? const_cast<unsigned long long*>(tile_slots) + range.x
                             : n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
@@ -1344,6 +1424,104 @@ struct GStage {  // one staged blend record (see gs_preprocess_one)
   float4 a, b, c;
 };
 
+// ---- spilled tiles --------------------------------------------------------------------------------
+// A tile whose pairs the front end could not all store (fused: more than its row's scap pairs, e.g.
+// the camera moved closer than the previous frame that sized the rows; three launches: a segment that
+// ends beyond the pair buffer sized from earlier frames) is completed by its own blend workgroup, in
+// the same launch: the front-end workgroups whose bounding rect (crect) holds the tile are listed,
+// their Gaussians' stored rects tested against the tile, and the keys (depth << 32 | gaussian, the
+// front ends' keys) collected; then sorted (bitonic: in the LDS arena up to GS_SPILL_LDS keys, else in
+// the pool) and the sorted gaussians written to the spill pool, from which the blend streams them like
+// a large tile's. Same keys, same order, same blend: the image equals a frame whose rows had fit (and
+// the oracle's). The pool (cap pairs per workspace) is reserved per tile with one atomic (fz[8], re-armed
+// by the next frame's front end, which also hands the demand to the host to size the pool); a tile that
+// does not fit is left at the background and counted (fz[10]; k_host[9] = 1: the next call reports it).
+struct GsSpill {
+  uint32_t* fz;                   // device counters: [8] pool cursor, [9] spilled tiles, [10] incomplete tiles
+  uint32_t* k_host;               // pinned host words: [9] <- 1 when a tile could not be completed
+  unsigned long long* keys;       // pool: keys of tiles above GS_SPILL_LDS pairs
+  uint32_t* vals;                 // pool: sorted gaussians of every spilled tile
+  uint32_t cap;                   // pool capacity (pairs)
+  const ushort4* crect;           // per front-end workgroup (chunk c of band b at c * bands + b): rect of its pairs
+  uint32_t nwg, bands, chunk, n;  // front-end workgroups, bands, Gaussians per chunk, Gaussians
+  const ushort4* rects;           // per Gaussian (walk order): tile rect (empty: culled)
+  const float* depths;            // per Gaussian (walk order): view depth
+  const uint32_t* ids;            // the caller's index (NULL: the walk index)
+};
+#define GS_SPILL_LDS 1984u  // keys sorted in the blend's LDS arena (15 872 B + the candidate list + counters)
+#define GS_SPILL_CAND 128u  // front-end workgroups tested per round
+
+// Returns the sorted gaussians of tile (tx, ty) in the pool and their count in m (on entry: the
+// tile's pair count), or nullptr when the pool is exhausted. Uses the arena (>= 16 400 B of LDS).
+__device__ const uint32_t* gs_spill_tile(const GsSpill& sp, uint32_t tx, uint32_t ty, uint32_t& m, char* arena) {
+  const uint32_t tid = threadIdx.x, n = m;
+  unsigned long long* s_k = reinterpret_cast<unsigned long long*>(arena);
+  uint32_t* s_c = reinterpret_cast<uint32_t*>(arena + 8 * GS_SPILL_LDS);
+  uint32_t* s_w = s_c + GS_SPILL_CAND;  // [0] keys found, [1] pool offset, [2] candidates of the round
+  const bool lds = n <= GS_SPILL_LDS;
+  if (tid == 0) {
+    s_w[0] = 0;
+    s_w[2] = 0;
+    uint32_t off = atomicAdd(sp.fz + 8, n);
+    atomicAdd(sp.fz + 9, 1u);
+    if (off > sp.cap || n > sp.cap - off) {
+      off = 0xFFFFFFFFu;
+      atomicAdd(sp.fz + 10, 1u);
+      __atomic_store_n(sp.k_host + 9, 1u, __ATOMIC_RELAXED);
+      __threadfence_system();
+    }
+    s_w[1] = off;
+  }
+  __syncthreads();
+  const uint32_t off = s_w[1];
+  if (off == 0xFFFFFFFFu) return nullptr;
+  unsigned long long* gk = sp.keys + off;
+  for (uint32_t w0 = 0; w0 < sp.nwg; w0 += GS_SPILL_CAND) {
+    if (tid < GS_SPILL_CAND && w0 + tid < sp.nwg) {
+      const ushort4 r = sp.crect[w0 + tid];
+      if (r.x <= tx && tx < r.z && r.y <= ty && ty < r.w) s_c[atomicAdd(s_w + 2, 1u)] = w0 + tid;
+    }
+    __syncthreads();
+    const uint32_t nc = s_w[2];
+    for (uint32_t k = 0; k < nc; ++k) {
+      const uint32_t c = s_c[k] / sp.bands;
+      const uint32_t g0 = c * sp.chunk, g1 = min(sp.n, g0 + sp.chunk);
+      for (uint32_t i = g0 + tid; i < g1; i += GS_BLOCK) {
+        const ushort4 r = sp.rects[i];
+        if (r.x <= tx && tx < r.z && r.y <= ty && ty < r.w) {
+          const unsigned long long key =
+              ((unsigned long long)__float_as_uint(sp.depths[i]) << 32) | (sp.ids ? sp.ids[i] : i);
+          const uint32_t p = atomicAdd(s_w, 1u);
+          if (p < n) {
+            if (lds) s_k[p] = key;
+            else gk[p] = key;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) s_w[2] = 0;
+    __syncthreads();
+  }
+  m = min(s_w[0], n);  // (= n: the rects are the ones the front end counted)
+  const uint32_t mm = m;
+  if (lds) {
+    bitonic_flip_sort(mm, [&](uint32_t a, uint32_t b) {
+      const unsigned long long x = s_k[a], y = s_k[b];
+      if (y < x) { s_k[a] = y; s_k[b] = x; }
+    });
+    for (uint32_t k = tid; k < mm; k += GS_BLOCK) sp.vals[off + k] = (uint32_t)s_k[k];
+  } else {
+    bitonic_flip_sort(mm, [&](uint32_t a, uint32_t b) {
+      const unsigned long long x = gk[a], y = gk[b];
+      if (y < x) { gk[a] = y; gk[b] = x; }
+    });
+    for (uint32_t k = tid; k < mm; k += GS_BLOCK) sp.vals[off + k] = (uint32_t)gk[k];
+  }
+  __syncthreads();  // the values (and the arena's last reads) before the blend stages records over them
+  return sp.vals + off;
+}
+
 // One 256-work-item workgroup per 16x16 tile (a persistent, software-pipelined variant that loads
 // the next tile's keys during the current one measured slower: static tile assignment loses to the
 // dispatcher's dynamic balancing, 103 vs 72 us at C2; a tile-pair workgroup shading two pixels per
@@ -1375,12 +1553,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
                                                                  uint32_t* __restrict__ vals_out,
                                                                  const float4* __restrict__ rec, float bg_r,
                                                                  float bg_g, float bg_b,
-                                                                 const uint32_t* __restrict__ total, uint32_t cap,
-                                                                 uint32_t slot_keys,
+                                                                 uint32_t cap, uint32_t slot_keys,
                                                                  const unsigned long long* __restrict__ tile_slots,
                                                                  const float* __restrict__ depth_lim,
                                                                  const float4* __restrict__ under,
-                                                                 float4* __restrict__ out, GsFused fu) {
+                                                                 float4* __restrict__ out, GsFused fu, GsSpill sp) {
   // staged records of the current batch; slot GS_BLOCK is a null Gaussian (alpha = 0) that pads the
   // per-quadrant lists to a multiple of 4.
   __shared__ __attribute__((aligned(16))) char s_arena[GS_ARENA];
@@ -1396,7 +1573,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   if (fu.scap) {
     // fused front end: block (0, 0) hands the frame's counters to the host and re-arms them (the
     // fused kernel that produced them has finished; no other blend block reads them)
-    const bool ovf = __hip_atomic_load(fu.fz + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fu.seq;
     uint32_t fp = 0, fr = 0;  // the front end's pairs and reservations (block (0, 0) sums the partials)
     if (blockIdx.x == 0 && blockIdx.y == 0) {
       for (uint32_t k = tid; k < fu.nwg; k += GS_BLOCK) {
@@ -1422,20 +1598,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       __atomic_store_n(fu.k_host + 1, big > 256u ? big : 256u, __ATOMIC_RELAXED);  // largest tile (bound)
       __atomic_store_n(fu.k_host + 2, fu.fz[4], __ATOMIC_RELAXED);                  // large tiles
       __atomic_store_n(fu.k_host + 4, fr, __ATOMIC_RELAXED);                        // reservations
-      __atomic_store_n(fu.k_host + 5, ovf ? 1u : 0u, __ATOMIC_RELAXED);            // tile above scap
+      __atomic_store_n(fu.k_host + 5, fu.fz[5], __ATOMIC_RELAXED);                  // tiles above scap (spilled)
       __atomic_store_n(fu.k_host + 6, 1u, __ATOMIC_RELAXED);                       // published by: fused
-      if (ovf) __atomic_store_n(fu.k_host + 3, __atomic_load_n(fu.k_host + 3, __ATOMIC_RELAXED) + 1u, __ATOMIC_RELAXED);
       __atomic_store_n(fu.k_host, fp, __ATOMIC_RELAXED);
       fu.fz[1] = 0;
       fu.fz[4] = 0;
+      fu.fz[5] = 0;
       __threadfence_system();
     }
-    if (ovf) {  // a tile did not fit its row: the frame is skipped (counted); cursors re-armed
-      if (tid == 0) fu.cursor[(cam.row_begin + blockIdx.y) * cam.grid_x + blockIdx.x] = 0;
-      return;
-    }
-  } else if (*total > cap) {
-    return;  // pair buffer too small this frame: the host re-runs after growing it
   }
 #if GS_XCD_REMAP
   // XCD-aware: the workgroups of one XCD blend one horizontal strip of tiles, so the records of the
@@ -1487,11 +1657,24 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   } else {
     range = ranges[tile];
   }
-  const uint32_t n = range.y - range.x;
+  uint32_t n = range.y - range.x;
 #endif
+  const uint32_t n_front = n;  // (the front end's count: n becomes the completed count of a spilled tile)
   const bool small = slot_keys && n <= GS_BLOCK;
   if (fu.scap && tid == 0) fu.ranges[tile] = range;
-  const bool mid = !small && n <= sorted_above;  // not sorted by gs_sort_large_kernel: sorted here
+  // a tile whose pairs were not all stored (fused: above its row's capacity; three launches: its
+  // segment ends beyond the pair buffer) is gathered and sorted here: its sorted gaussians come from
+  // the spill pool (nullptr: pool exhausted, the tile stays at the background; counted)
+  const bool spilled = fu.scap ? n > fu.scap : (n > GS_TILE_SLOTS && range.y > cap);
+  const uint32_t* vsrc = vals_out + range.x;
+  if (spilled) {
+    vsrc = gs_spill_tile(sp, tile_x, tile_y, n, s_arena);
+    if (!vsrc) n = 0;
+  }
+  const bool mid = !small && !spilled && n <= sorted_above;  // not sorted by gs_sort_large_kernel: sorted here
+  // publish (PTGS_FLAG_SPLAT_PUBLISH) only where the tile's range fits the buffers: a three-launch frame
+  // above the pair buffer is re-run by the host after growing them (the published layout is that run's)
+  const bool pub = keys_out && (fu.scap || range.y <= cap);
   const bool mid_lds = mid && n <= GS_MID;
   const unsigned long long tbits = (unsigned long long)tile << 32;
   float4 ra, rb, rc;     // records in flight: the unsorted keys' (small) / batch b + 1's (large)
@@ -1534,7 +1717,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     __syncthreads();  // every read of the keys is done before records overwrite them
     if (tid < n) s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
     if (sk != ~0ull) {
-      if (keys_out) {
+      if (pub) {
         keys_out[range.x + r] = tbits | (sk >> 32);
         vals_out[range.x + r] = (uint32_t)(sk >> 8) & 0xFFFFFFu;
       }
@@ -1566,7 +1749,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     __syncthreads();  // every read of the keys is done before records overwrite them
     if (tid < n) {
       s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
-      if (keys_out) {
+      if (pub) {
         keys_out[range.x + r] = tbits | (key >> 32);
         vals_out[range.x + r] = (uint32_t)(key >> 8) & 0xFFFFFFu;
       }
@@ -1603,7 +1786,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     if (npad >= 128) __syncthreads();  // the last exchange reads are done before records overwrite them
     if (tid < n) {
       s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
-      if (keys_out) {  // published frame only (PTGS_FLAG_SPLAT_PUBLISH): the blend needs neither
+      if (pub) {  // published frame only (PTGS_FLAG_SPLAT_PUBLISH): the blend needs neither
         keys_out[range.x + tid] = tbits | (key >> 32);
         vals_out[range.x + tid] = (uint32_t)(key >> 8) & 0xFFFFFFu;
       }
@@ -1653,7 +1836,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         if (k0 != ~0ull) s_key[r0] = k0;  // (the slots below n hold exactly the keys other than ~0)
         if (k1 != ~0ull) s_key[r1] = k1;
         __syncthreads();
-        if (keys_out)
+        if (pub)
           for (uint32_t k = tid; k < n; k += GS_BLOCK) {
             const unsigned long long v = s_key[k];
             keys_out[range.x + k] = tbits | (v >> 32);
@@ -1666,7 +1849,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         });
         for (uint32_t k = tid; k < n; k += GS_BLOCK) {
           const unsigned long long v = seg[k];
-          if (keys_out) keys_out[range.x + k] = tbits | (v >> 32);
+          if (pub) keys_out[range.x + k] = tbits | (v >> 32);
           vals_out[range.x + k] = (uint32_t)v;
         }
         __syncthreads();
@@ -1674,12 +1857,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     }
     // sorted values (LDS for mid tiles, else vals_out): batch 0's records and batch 1's values in flight
     if (tid < n) {
-      const uint32_t g = mid_lds ? (uint32_t)s_key[tid] : vals_out[range.x + tid];
+      const uint32_t g = mid_lds ? (uint32_t)s_key[tid] : vsrc[tid];
       ra = rec[3 * g];
       rb = rec[3 * g + 1];
       rc = rec[3 * g + 2];
     }
-    if (tid + GS_BLOCK < n) g_next = mid_lds ? (uint32_t)s_key[tid + GS_BLOCK] : vals_out[range.x + tid + GS_BLOCK];
+    if (tid + GS_BLOCK < n) g_next = mid_lds ? (uint32_t)s_key[tid + GS_BLOCK] : vsrc[tid + GS_BLOCK];
   }
   if (tid == 0) {  // the null record (alpha 0) that pads the per-quadrant lists
     s_stage[GS_BLOCK].a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1716,7 +1899,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         rb = rec[3 * g + 1];
         rc = rec[3 * g + 2];
       }
-      if (idx + 2 * GS_BLOCK < n) g_next = vals_out[range.x + idx + 2 * GS_BLOCK];
+      if (idx + 2 * GS_BLOCK < n) g_next = vsrc[idx + 2 * GS_BLOCK];
       __syncthreads();  // the batch's records and masks are staged
     }
     // each wave compacts its own quadrant's list from every staged mask, in sorted order (no
@@ -1786,7 +1969,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     }
   }
   STAMP(1, 2);
-  if (fu.scap && tid == 0 && n) fu.cursor[tile] = 0;  // (n > 0: every wave passed a barrier after reading it)
+  if (fu.scap && tid == 0 && n_front) fu.cursor[tile] = 0;  // (n > 0: every wave passed a barrier after reading it)
   if (inside) {
     // the pixel index is recomputed here from a laundered thread id, so that the one computed before
     // the batch loop is not kept (spilled) across it
@@ -1812,14 +1995,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
 // (exclusive scan of the tile counts -> ranges, empty tiles (0, 0)) so both paths publish alike.
 // Unpublished fused frames leave ranges[t] = (t * scap, t * scap + n): end - begin is the count.
 #define GS_PUB_THREADS 1024
+// (a spilled tile's count exceeds its row: only the row's scap keys are copied; a published frame with
+// spilled tiles is re-run through the three-launch path by the host)
 __global__ __launch_bounds__(GS_PUB_THREADS) void gs_publish_scan_kernel(const uint2* __restrict__ fr, uint32_t ntiles,
-                                                                         uint32_t t_begin, uint32_t t_end,
+                                                                         uint32_t t_begin, uint32_t t_end, uint32_t scap,
                                                                          uint32_t* __restrict__ offs) {
   __shared__ uint32_t s_part[GS_PUB_THREADS / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t per = (ntiles + GS_PUB_THREADS - 1) / GS_PUB_THREADS, a = tid * per, b = min(ntiles, a + per);
   uint32_t sum = 0;
-  for (uint32_t t = a; t < b; ++t) sum += (t >= t_begin && t < t_end) ? fr[t].y - fr[t].x : 0u;
+  for (uint32_t t = a; t < b; ++t) sum += (t >= t_begin && t < t_end) ? min(scap, fr[t].y - fr[t].x) : 0u;
   const uint32_t incl = wave_incl_scan(sum);
   if (lane == 63) s_part[wv] = incl;
   __syncthreads();
@@ -1827,12 +2012,12 @@ __global__ __launch_bounds__(GS_PUB_THREADS) void gs_publish_scan_kernel(const u
   for (uint32_t w = 0; w < wv; ++w) run += s_part[w];
   for (uint32_t t = a; t < b; ++t) {
     offs[t] = run;
-    run += (t >= t_begin && t < t_end) ? fr[t].y - fr[t].x : 0u;
+    run += (t >= t_begin && t < t_end) ? min(scap, fr[t].y - fr[t].x) : 0u;
   }
 }
 
 __global__ __launch_bounds__(256) void gs_publish_copy_kernel(const uint2* __restrict__ fr, const uint32_t* __restrict__ offs,
-                                                              uint32_t t_begin, uint32_t t_end,
+                                                              uint32_t t_begin, uint32_t t_end, uint32_t scap,
                                                               const unsigned long long* __restrict__ keys_in,
                                                               const uint32_t* __restrict__ vals_in,
                                                               unsigned long long* __restrict__ keys_out,
@@ -1840,7 +2025,7 @@ __global__ __launch_bounds__(256) void gs_publish_copy_kernel(const uint2* __res
   const uint32_t t = blockIdx.x;
   const bool in = t >= t_begin && t < t_end;
   const uint2 r = in ? fr[t] : make_uint2(0u, 0u);
-  const uint32_t n = r.y - r.x, o = offs[t];
+  const uint32_t n = min(scap, r.y - r.x), o = offs[t];
   __syncthreads();  // (ranges may be fr itself: every work-item has read fr[t])
   if (threadIdx.x == 0) ranges[t] = n ? make_uint2(o, o + n) : make_uint2(0u, 0u);
   for (uint32_t k = threadIdx.x; k < n; k += 256) {
@@ -1852,8 +2037,10 @@ __global__ __launch_bounds__(256) void gs_publish_copy_kernel(const uint2* __res
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
-                           ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s) {
+                           ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s,
+                           uint32_t* report) {
   hipError_t e;
+  *report = 0;
   if (time_stages && !w->ev[0])
     for (hipEvent_t& ev : w->ev)
       if ((e = hipEventCreate(&ev))) return e;
@@ -1918,6 +2105,33 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     std::memset(w->k_host, 0, 64);
     if ((e = hipHostGetDevicePointer((void**)&w->k_dev, w->k_host, 0))) return e;
   }
+  if (!w->fz.p) {  // device counters of both front ends, the blend and the spill pool (zero once)
+    if ((e = ensure(w->fz, 64))) return e;
+    if ((e = hipMemsetAsync(w->fz.p, 0, 64, s))) return e;
+  }
+  // An earlier frame of this workspace left a spilled tile incomplete (pool exhausted; k_host[9], a
+  // device store seen once that frame has run) or met an id >= N (k_host[10]): reported by this call,
+  // which renders its own frame after growing the pool (splat_common maps it to PTGS_EINCOMPLETE /
+  // PTGS_EINVAL). A call with stats waits for the earlier frames first (it is synchronous anyway), so
+  // their reports are its own and the flags its superseded runs may raise can be dropped below.
+  if (stats && (e = hipStreamSynchronize(s))) return e;
+  if (__atomic_exchange_n(w->k_host + 9, 0u, __ATOMIC_ACQ_REL)) {
+    ++w->incomplete;
+    *report |= 1u;
+  }
+  if (__atomic_exchange_n(w->k_host + 10, 0u, __ATOMIC_ACQ_REL)) *report |= 2u;
+  // Spill pool: at least max(2^20, N) pairs, the reservation, and 1.25x the demand of the latest
+  // frame whose front end has run (k_host[8]; a hint, no wait). Growth frees the old pool (waits).
+  {
+    const uint32_t demand = w->k_host[8];
+    uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1u << 20, n), w->sp_cap);
+    if (demand > w->sp_cap) want = std::max<uint64_t>(want, (uint64_t)demand + demand / 4u);
+    want = std::min<uint64_t>(want, 0xFFFFFFF0u);
+    if (want > w->sp_cap || !w->sp_keys.p) {
+      if ((e = ensure(w->sp_keys, want * 8)) || (e = ensure(w->sp_vals, want * 4))) return e;
+      w->sp_cap = (uint32_t)std::min<size_t>(std::min(w->sp_keys.bytes / 8, w->sp_vals.bytes / 4), 0xFFFFFFF0u);
+    }
+  }
 #ifndef GS_K_EVENT_FLAGS
 #define GS_K_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
 #endif
@@ -1965,6 +2179,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   pa.rec = (float4*)w->rec.p;
   pa.ids = g->ids;
   pa.dbg_depths = (float*)w->dbg_depths.p;
+  pa.bad_ids = w->k_dev + 10;
   if (!publish) {  // the per-Gaussian debug outputs only for a published frame (ptgs_splat_get_buffers)
     pa.radii = nullptr;
     pa.touched = nullptr;
@@ -2009,14 +2224,35 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if (big <= GS_FUSED_MAX_SCAP && (size_t)tiles * c * 8 <= ((size_t)4 << 30)) scap = c;
   }
   const uint32_t rows = cam.row_end - cam.row_begin;
+  // per front-end workgroup chunk rects (gs_spill_tile): fused (bands x 256-Gaussian chunks) or count
+  const uint32_t nwg_fused = bgrid.bands * ((n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS);
+  if ((e = ensure(w->crect, (size_t)std::max(nwg_fused, bgrid.bands * bgrid.chunks) * 8))) return e;
+  auto spill_args = [&](bool fused_fe) -> GsSpill {
+    GsSpill sp;
+    sp.fz = (uint32_t*)w->fz.p;
+    sp.k_host = w->k_dev;
+    sp.keys = (unsigned long long*)w->sp_keys.p;
+    sp.vals = (uint32_t*)w->sp_vals.p;
+    sp.cap = w->sp_cap;
+    sp.crect = (const ushort4*)w->crect.p;
+    sp.bands = bgrid.bands;
+    sp.chunk = fused_fe ? GS_FUSED_THREADS : bgrid.chunk;
+    sp.nwg = fused_fe ? nwg_fused : bgrid.bands * bgrid.chunks;
+    sp.n = n;
+    sp.rects = (const ushort4*)w->rect.p;
+    sp.depths = (const float*)w->depths.p;
+    sp.ids = g->ids;
+    return sp;
+  };
   auto blend = [&](uint32_t cap, const GsFused& fu, unsigned long long* keys_out, bool sort_large) -> hipError_t {
     if (rows == 0) return hipSuccess;
     auto k = depth ? gs_sort_blend_kernel<true> : gs_sort_blend_kernel<false>;
     const dim3 grid(cam.grid_x, rows);
     hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
                        sort_large ? (uint32_t)GS_MID : 0xFFFFFFFFu, keys_out, (uint32_t*)w->vals_out.p,
-                       (const float4*)w->rec.p, bg[0], bg[1], bg[2], (const uint32_t*)w->total.p, cap, slot_keys,
-                       (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out, fu);
+                       (const float4*)w->rec.p, bg[0], bg[1], bg[2], cap, slot_keys,
+                       (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out, fu,
+                       spill_args(fu.scap != 0));
     return hipGetLastError();
   };
   auto sort_attr = [&]() -> hipError_t {
@@ -2035,7 +2271,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     order = (uint32_t*)w->order.p;
   }
 #endif
-  const GsFused no_fu = {0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order};
+  const GsFused no_fu = {0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order};
 
   auto enqueue_fused = [&]() -> hipError_t {
     hipError_t e2;
@@ -2046,25 +2282,21 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
       if ((e2 = ensure(w->cursor, (size_t)tiles * 4))) return e2;
       if ((e2 = hipMemsetAsync(w->cursor.p, 0, w->cursor.bytes, s))) return e2;
     }
-    if (!w->fz.p) {
-      if ((e2 = ensure(w->fz, 64))) return e2;
-      if ((e2 = hipMemsetAsync(w->fz.p, 0, 64, s))) return e2;
-    }
-    const uint32_t nwg = bgrid.bands * ((n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS);
+    const uint32_t nwg = nwg_fused;
     if ((e2 = ensure(w->fzp, (size_t)nwg * 8))) return e2;
-    const uint32_t seq = ++w->seq;
-    GsFused fu = {scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
+    GsFused fu = {scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
                   (uint32_t*)w->fzp.p, nwg, order};
-    PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers
+    PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers (band 0 stores them for gs_spill_tile)
     fpa.rects = nullptr;
     fpa.depths = nullptr;
     BinGrid fg = bgrid;
     fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
     fg.chunk = GS_FUSED_THREADS;
     hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks + (order ? 1u : 0u)), dim3(GS_FUSED_WG), band_lds, s,
-                       cam, fpa, fg, scap, seq, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
+                       cam, fpa, fg, scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
                        (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, order,
-                       cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x);
+                       cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x, (ushort4*)w->crect.p, (ushort4*)w->rect.p,
+                       (float*)w->depths.p, w->k_dev);
     if ((e2 = hipGetLastError())) return e2;
     if ((e2 = mark(1)) || (e2 = mark(2)) || (e2 = mark(3))) return e2;
     unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
@@ -2087,9 +2319,9 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
       if ((e2 = ensure(w->vals_pub, (size_t)tiles * scap * 4))) return e2;
       const uint32_t tb = cam.row_begin * cam.grid_x, te = cam.row_end * cam.grid_x;
       hipLaunchKernelGGL(gs_publish_scan_kernel, dim3(1), dim3(GS_PUB_THREADS), 0, s, (const uint2*)w->ranges.p, tiles,
-                         tb, te, (uint32_t*)w->pub_offs.p);
+                         tb, te, scap, (uint32_t*)w->pub_offs.p);
       hipLaunchKernelGGL(gs_publish_copy_kernel, dim3(tiles), dim3(256), 0, s, (const uint2*)w->ranges.p,
-                         (const uint32_t*)w->pub_offs.p, tb, te, (const unsigned long long*)w->keys_out.p,
+                         (const uint32_t*)w->pub_offs.p, tb, te, scap, (const unsigned long long*)w->keys_out.p,
                          (const uint32_t*)w->vals_out.p, (unsigned long long*)w->keys_pub.p, (uint32_t*)w->vals_pub.p,
                          (uint2*)w->ranges.p);
       if ((e2 = hipGetLastError())) return e2;
@@ -2143,7 +2375,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks + (order ? 1u : 0u)), dim3(GS_COUNT_THREADS),
                        std::max(band_lds, (size_t)GS_ORDER_BUCKETS * 4), s, cam, pa, bgrid, (uint32_t*)w->hist.p,
                        (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev, (uint32_t*)w->nzbuf.p,
-                       (const uint2*)w->ranges.p, order, cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x);
+                       (const uint2*)w->ranges.p, order, cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x,
+                       (uint32_t*)w->fz.p, (ushort4*)w->crect.p);
     if ((e2 = hipGetLastError())) return e2;
     if ((e2 = mark(1))) return e2;
     hipLaunchKernelGGL(gs_bin_colscan_kernel, dim3(bgrid.groups), dim3(GS_COLSCAN_THREADS), 0, s, bgrid, (uint32_t*)w->hist.p,
@@ -2163,21 +2396,25 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = hipEventSynchronize(w->k_event))) return e;
     K = w->k_host[0];
     // a fused frame with a tile above its row capacity, or a three-launch frame above the pair
-    // buffer, was skipped on the device (and counted): this call re-runs it so that it is complete
-    // (uncounted again: every earlier frame of this workspace has finished, so no device write of
-    // the word is pending)
+    // buffer, was completed through the spill pool; a call with stats re-runs it so that its published
+    // keys / values / ranges are the exact layout (three launches, grown buffers)
     if (fused && w->k_host[5]) {
-      if (w->k_host[3]) w->k_host[3] -= 1u;
       redone = true;
       if ((e = mark(0)) || (e = enqueue_three())) return e;
       if ((e = hipEventSynchronize(w->k_event))) return e;
       K = w->k_host[0];
     }
+    bool regrown = false;
     if ((!fused || redone) && K > cap_now()) {
-      if (w->k_host[3]) w->k_host[3] -= 1u;
       if ((e = grow(K))) return e;
       if ((e = mark(2))) return e;
       if ((e = enqueue_tail(cap_now()))) return e;
+      regrown = true;
+    }
+    if (redone || regrown) {  // the superseded run's spilled tiles may have exhausted the pool: the
+                              // re-run completed the frame, so its report is dropped
+      if ((e = hipStreamSynchronize(s))) return e;
+      __atomic_store_n(w->k_host + 9, 0u, __ATOMIC_RELEASE);
     }
     stats->num_rendered = K;
     stats->tiles_x = cam.grid_x;
@@ -2307,20 +2544,43 @@ hipError_t splat_sort_spatial(const ptgs_gaussians* g, float* means, float* scal
   return done(hipGetLastError());
 }
 
+// pairs: the pair buffer (three launches: a frame of K <= pairs stores every pair) and the spill pool
+// (fused rows: a frame's spilled tiles hold at most K pairs) — a frame of at most `pairs` pairs is always
+// rendered completely, whichever front end runs and whatever its row capacity (hipGraph replays too)
 hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs) {
   hipError_t e;
   if ((e = ensure(w->pairs, (size_t)pairs * 8))) return e;
   if ((e = ensure(w->vals_out, (size_t)pairs * 4))) return e;
   if (w->keys_out.p && (e = ensure(w->keys_out, (size_t)pairs * 8))) return e;
+  if (pairs > w->sp_cap) {
+    if ((e = ensure(w->sp_keys, (size_t)pairs * 8)) || (e = ensure(w->sp_vals, (size_t)pairs * 4))) return e;
+    w->sp_cap = (uint32_t)std::min<size_t>(std::min(w->sp_keys.bytes / 8, w->sp_vals.bytes / 4), 0xFFFFFFF0u);
+  }
   return hipSuccess;
 }
 
-void splat_status(SplatWorkspace* w, bool clear, uint32_t* skipped, uint32_t* capacity, uint32_t* last_pairs) {
-  *skipped = w->k_host ? w->k_host[3] : 0u;
-  if (clear && w->k_host) w->k_host[3] = 0u;
+hipError_t splat_status(SplatWorkspace* w, bool clear, SplatStatusOut* out) {
+  *out = SplatStatusOut{};
+  if (w->k_host && __atomic_exchange_n(w->k_host + 9, 0u, __ATOMIC_ACQ_REL)) ++w->incomplete;
+  out->incomplete = w->incomplete;
+  if (clear) w->incomplete = 0;
   const size_t c = std::min(w->pairs.bytes / 8, w->vals_out.bytes / 4);
-  *capacity = (uint32_t)std::min<size_t>(c, 0xFFFFFFFFu);
-  *last_pairs = w->k_host ? w->k_host[0] : 0u;
+  out->capacity = (uint32_t)std::min<size_t>(c, 0xFFFFFFFFu);
+  out->last_pairs = w->k_host ? w->k_host[0] : 0u;
+  out->spill_capacity = w->sp_cap;
+  if (w->fz.p) {  // device counters (the caller has drained the workspace's stream)
+    uint32_t fz[16];
+    const hipError_t e = hipMemcpy(fz, w->fz.p, sizeof(fz), hipMemcpyDeviceToHost);
+    if (e) return e;
+    out->spilled_tiles = fz[9] - w->spilled_base;
+    out->incomplete_tiles = fz[10] - w->incomplete_base;
+    out->spill_demand = std::max(fz[8], fz[11]);
+    if (clear) {
+      w->spilled_base = fz[9];
+      w->incomplete_base = fz[10];
+    }
+  }
+  return hipSuccess;
 }
 
 uint32_t splat_pair_hint(const SplatWorkspace* w) { return w->k_host ? w->k_host[0] : 0u; }

@@ -269,13 +269,15 @@ class Renderer:
 
     def splat_status(self, stream=None) -> SplatStatus:
         """ptgs_splat_status_read: waits for `stream` and the view streams, returns and clears the
-        count of splat frames skipped because their pair count exceeded the pair buffer."""
+        counts since the last query: frames left incomplete (spill pool exhausted), tiles completed
+        through the spill pool, tiles left incomplete; buffer capacities."""
         st = SplatStatus()
         self._chk(self.lib.ptgs_splat_status_read(self._h, C.byref(st), _stream(stream)), "ptgs_splat_status_read")
         return st
 
     def splat_reserve(self, pairs: int):
-        """Grow every view slot's pair buffer to at least `pairs` (no skipped frames up to that count)."""
+        """Grow every view slot's pair buffer and spill pool to at least `pairs` (frames of up to that
+        many pairs are always complete)."""
         self._chk(self.lib.ptgs_splat_reserve(self._h, int(pairs)), "ptgs_splat_reserve")
 
     def bvh_buffers(self) -> BvhBuffers:

@@ -33,12 +33,15 @@ def test_every_declared_symbol_is_exported(native_lib):
 
 
 def test_abi_version_and_arch(native_lib):
-    assert native_lib.ptgs_abi_version() == 2
+    assert native_lib.ptgs_abi_version() == 3  # 3: ids / fused / the splat status's spill fields
     assert native_lib.ptgs_device_arch() == b"gfx950"
 
 
 def test_struct_layouts():
     from pathtracer_gaussiansplatting_amd import _abi
+    # ptgs_splat_status (ABI 3): frames u64, views[8], 4 x u32, spilled / incomplete tiles u64, 2 x u32
+    st = _abi.SplatStatus
+    assert C.sizeof(st) == 80 and st.spilled_tiles.offset == 56 and st.spill_demand.offset == 76
     # Appendix B sizes / offsets
     assert _abi.VERTEX_DTYPE.itemsize == 80
     assert _abi.VERTEX_DTYPE.fields["normal"][1] == 16 and _abi.VERTEX_DTYPE.fields["tex_coord"][1] == 64

@@ -1,0 +1,277 @@
+"""The stream-ordered 3DGS splat behind a moving camera: PTGS_OK must mean a
+rendered frame. The reference's viewer renders a new view every frame (camera.cpp:11,
+engine.cpp:2070-2072); the splat sizes its per-tile rows, its pair buffer and its tile order from
+earlier frames, so a camera that moves closer than the previous frame outgrows them. Those tiles are
+completed on the device through the spill pool (gs_spill_tile): every frame here must equal the exact
+(stats, re-run) frame bit for bit - whose published keys / values / ranges are the oracle's - and the
+oracle's image within 1e-4 relative L2.
+"""
+import numpy as np
+import pytest
+
+import scenes_util as U
+from pathtracer_gaussiansplatting_amd import Camera, make_ubo
+from pathtracer_gaussiansplatting_amd import synthetic as Y
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _read(renderer, ptr, n, dtype):
+    out = np.zeros(n, dtype)
+    if n:
+        renderer.copy_d2h(out, ptr, out.nbytes)
+    return out
+
+
+def orbit_ubo(k, W, H, radius=None, sc=None):
+    """Frame k of an orbit around the C2 cloud's centre (0, 0, -8) with a slow dolly-in; frame k = 0 is
+    the C2 camera (origin, looking down -Z)."""
+    r = 8.0 - 0.2 * k if radius is None else radius
+    th = np.radians(4.0 * k)
+    c = np.array([0.0, 0.0, -8.0])
+    eye = c + np.array([r * np.sin(th), 0.15 * r * np.sin(0.5 * th), r * np.cos(th)])
+    pose = Camera(aspect=W / H).look_at(eye.tolist(), c.tolist())
+    return make_ubo(pose, U.cornell() if sc is None else sc, 0)
+
+
+def _exact(r2, dg, ubo, W, H, oracle_lib, g, bg=(0.0, 0.0, 0.0)):
+    """The exact frame: stats (a frame that spilled is re-run through three launches with grown
+    buffers) + published keys / values / ranges, checked against the oracle."""
+    out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    st = r2.splat_gaussians(dg, ubo, W, H, out, bg=bg, want_stats=True)
+    torch.cuda.synchronize()
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H, bg=bg)
+    b = r2.splat_buffers()
+    assert st.num_rendered == ref["K"]
+    np.testing.assert_array_equal(_read(r2, b.sorted_keys, ref["K"], np.uint64), ref["keys"])
+    np.testing.assert_array_equal(_read(r2, b.sorted_values, ref["K"], np.uint32), ref["vals"])
+    np.testing.assert_array_equal(_read(r2, b.tile_ranges, 2 * b.num_tiles, np.uint32), ref["ranges"])
+    err = U.rel_l2(out.cpu().numpy(), ref["image"])
+    assert err < 1e-4, err
+    return out, ref
+
+
+def test_gaussians_moving_camera_sequence(native_lib, oracle_lib):
+    """An orbiting, dollying camera over 20k C2 Gaussians (Morton copy with ids: the fused front end,
+    rows sized from the previous frame), with one sudden zoom out that grows the densest tile far past
+    its row (into the pool-sorted spill path): every stream-ordered frame (no
+    stats) equals the exact frame bit for bit (keys / values / ranges of the exact frame = the
+    oracle's), no frame is incomplete, and the zoom frame spilled."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H, n = 480, 270, 20_000
+    g = Y.gaussians_c2(n, seed=31)
+    g["means"][1::59] = g["means"][0::59][: len(g["means"][1::59])]  # duplicated means: equal depths
+    # orbit + dolly-in, then a sudden dolly-out to 20 units (the whole cloud in a few hundred tiles:
+    # the densest tile grows from ~380 to ~2300 pairs, past the 512-pair rows sized from frame 7 and
+    # past the spill LDS sort), further out, then back into the orbit
+    frames = [orbit_ubo(k, W, H) for k in range(8)] + [orbit_ubo(8, W, H, radius=20.0)] + \
+             [orbit_ubo(k, W, H, radius=20.0 + 3.0 * (k - 8)) for k in range(9, 12)] + \
+             [orbit_ubo(k, W, H) for k in (12, 13)]
+    ra = Renderer(0)
+    rb = Renderer(0, publish_splat_buffers=True)
+    try:
+        da = ra.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        db = {k: _dev(v) for k, v in g.items()}
+        spilled = []
+        for k, ubo in enumerate(frames):
+            out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+            ra.splat_gaussians(da, ubo, W, H, out, bg=(0.1, 0.2, 0.3))  # stream-ordered
+            st = ra.splat_status()
+            assert st.frames == 0 and st.incomplete_tiles == 0, (k, st.frames, st.incomplete_tiles)
+            spilled.append(int(st.spilled_tiles))
+            exact, ref = _exact(rb, db, ubo, W, H, oracle_lib, g, bg=(0.1, 0.2, 0.3))
+            assert torch.equal(out, exact), f"frame {k}: stream-ordered != exact"
+        print("spilled tiles per frame:", spilled)
+        assert spilled[8] > 0, spilled  # the zoom outgrew the rows sized from frame 7
+        assert ra.splat_status().fused == 1
+    finally:
+        ra.close()
+        rb.close()
+
+
+def test_gaussians_timed_c2_mode_vs_oracle(native_lib, oracle_lib):
+    """The exact mode bench.py's C2 headline times: 100k Gaussians at 1920x1080, a Morton-ordered copy
+    with ids (ptgs_gaussians_sort_spatial), no stats, steady state (fused front end, rows and tile
+    order from the previous frame). Its frames equal the oracle's image (< 1e-4) and, bit for bit, the
+    exact published frame whose keys / values / ranges are the oracle's; nothing spills."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H, n = 1920, 1080, 100_000
+    g = Y.gaussians_c2(n, seed=1)
+    sc = U.cornell()
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), sc, 0)
+    ra = Renderer(0)
+    rb = Renderer(0, publish_splat_buffers=True)
+    try:
+        dg = ra.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        outs = []
+        for _ in range(4):  # frame 0: three launches; 1..3: fused, steady state
+            out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            ra.splat_gaussians(dg, ubo, W, H, out)
+            outs.append(out)
+        st = ra.splat_status()
+        assert st.fused == 1 and st.frames == 0 and st.spilled_tiles == 0, (st.fused, st.frames, st.spilled_tiles)
+        exact, ref = _exact(rb, {k: _dev(v) for k, v in g.items()}, ubo, W, H, oracle_lib, g)
+        for k, o in enumerate(outs):
+            assert torch.equal(o, exact), k
+        print(f"C2 timed mode: K={ref['K']}, rel L2 vs oracle {U.rel_l2(outs[-1].cpu().numpy(), ref['image']):.2e}")
+    finally:
+        ra.close()
+        rb.close()
+
+
+def test_gaussians_graph_replay_fused_spill(native_lib, oracle_lib):
+    """a hipGraph of a fused frame bakes its row capacity. Replays of that graph after the
+    Gaussians were made denser in place (tiles above the rows) must render completely through the
+    spill pool, and a later replay of the original data must render normally again (no stale state
+    left by the spilled replay)."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H, n = 320, 180, 20_000
+    s1 = Y.gaussians_c2(n, seed=41)
+    s2 = {k: v.copy() for k, v in s1.items()}
+    s2["means"][:, :2] *= np.float32(0.5)  # the cloud squeezed to half the width: tiles of up to ~3000
+                                           # pairs, above the 1024-pair rows sized from s1's ~800
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    ra = Renderer(0)
+    rb = Renderer(0, publish_splat_buffers=True)
+    try:
+        dg = ra.sort_gaussians_spatial({k: _dev(v) for k, v in s1.items()})
+        ids = dg["ids"].cpu().numpy().astype(np.int64)
+        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        for _ in range(3):
+            ra.splat_gaussians(dg, ubo, W, H, out, want_stats=True)
+        assert ra.splat_status().fused == 1
+        exact1, ref1 = _exact(rb, {k: _dev(v) for k, v in s1.items()}, ubo, W, H, oracle_lib, s1)
+        exact2, ref2 = _exact(rb, {k: _dev(v) for k, v in s2.items()}, ubo, W, H, oracle_lib, s2)
+        assert int(np.diff(ref2["ranges"].reshape(-1, 2), axis=1).max()) > \
+            2 * int(np.diff(ref1["ranges"].reshape(-1, 2), axis=1).max())
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ra.splat_gaussians(dg, ubo, W, H, out)
+
+        def load(src):
+            for k in ("means", "scales", "rotations", "opacities", "colors"):
+                dg[k].copy_(_dev(src[k][ids]))
+            torch.cuda.synchronize()
+
+        for data, exact in ((s1, exact1), (s2, exact2), (s1, exact1), (s2, exact2)):
+            load(data)
+            out.fill_(-7.0)
+            graph.replay()
+            torch.cuda.synchronize()
+            st = ra.splat_status()
+            assert st.frames == 0 and st.incomplete_tiles == 0
+            assert (st.spilled_tiles > 0) == (data is s2), st.spilled_tiles
+            assert torch.equal(out, exact)
+        del graph
+    finally:
+        ra.close()
+        rb.close()
+
+
+def test_gaussians_spill_tiles_beyond_lds(native_lib, oracle_lib):
+    """Spilled tiles of more than GS_SPILL_LDS (1984) pairs are sorted in the spill pool (global
+    bitonic) instead of the blend's LDS: 3000 screen-filling Gaussians at 128x72 on a fresh context
+    (every tile holds ~3000 pairs, K ~ 120k > the 8-per-Gaussian pair buffer)."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H = 128, 72
+    g = Y.gaussians_c2(3000, seed=43)
+    g["scales"] *= np.float32(40.0)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    ra = Renderer(0)
+    rb = Renderer(0, publish_splat_buffers=True)
+    try:
+        dg = {k: _dev(v) for k, v in g.items()}
+        out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+        ra.splat_gaussians(dg, ubo, W, H, out)
+        st = ra.splat_status()
+        exact, ref = _exact(rb, dg, ubo, W, H, oracle_lib, g)
+        per_tile = np.diff(ref["ranges"].reshape(-1, 2), axis=1).ravel()
+        assert per_tile.max() > 1984 and ref["K"] > 8 * 3000, (per_tile.max(), ref["K"])
+        assert st.frames == 0 and st.incomplete_tiles == 0 and st.spilled_tiles > 0
+        assert torch.equal(out, exact)
+    finally:
+        ra.close()
+        rb.close()
+
+
+def test_gaussians_spill_pool_exhausted_is_reported(native_lib):
+    """The only incomplete case: a frame whose spilled tiles need more than the spill pool (here ~16M
+    pairs on a fresh context: 2000 screen-filling Gaussians at 1920x1080 against an 8-per-Gaussian
+    pair buffer and a 2^20-pair pool). Its tiles beyond the pool stay at the background, and the next
+    call - after that frame finished - returns PTGS_EINCOMPLETE having grown the buffers and rendered
+    its own frame completely; ptgs_splat_reserve rules the case out beforehand."""
+    from pathtracer_gaussiansplatting_amd import Renderer, PtgsError
+    from pathtracer_gaussiansplatting_amd._abi import PTGS_EINCOMPLETE
+    W, H = 1920, 1080
+    g = Y.gaussians_c2(2000, seed=45)
+    g["scales"] *= np.float32(60.0)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    dg = {k: _dev(v) for k, v in g.items()}
+    rb = Renderer(0)
+    try:
+        exact = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        st = rb.splat_gaussians(dg, ubo, W, H, exact, want_stats=True)
+        K = st.num_rendered
+        assert K > (1 << 20) + 8 * 2000, K
+    finally:
+        rb.close()
+    ra = Renderer(0)
+    try:
+        out = torch.zeros_like(exact)
+        ra.splat_gaussians(dg, ubo, W, H, out)  # incomplete: its spilled tiles exceed the pool
+        torch.cuda.synchronize()
+        with pytest.raises(PtgsError) as ei:
+            ra.splat_gaussians(dg, ubo, W, H, out)  # reports the earlier frame; renders its own
+        assert ei.value.code == PTGS_EINCOMPLETE
+        torch.cuda.synchronize()
+        st = ra.splat_status()
+        assert st.frames == 1 and st.incomplete_tiles > 0, (st.frames, st.incomplete_tiles)
+        assert torch.equal(out, exact)  # the reporting call's own frame is complete
+        ra.splat_gaussians(dg, ubo, W, H, out)  # nothing more to report
+        st = ra.splat_status()
+        assert st.frames == 0 and st.incomplete_tiles == 0 and torch.equal(out, exact)
+    finally:
+        ra.close()
+    rc = Renderer(0)
+    try:
+        rc.splat_reserve(K)  # reserved: the first stream-ordered frame is complete
+        out = torch.zeros_like(exact)
+        rc.splat_gaussians(dg, ubo, W, H, out)
+        st = rc.splat_status()
+        assert st.frames == 0 and st.incomplete_tiles == 0 and torch.equal(out, exact)
+    finally:
+        rc.close()
+
+
+def test_gaussians_out_of_range_ids_are_reported(native_lib, oracle_lib):
+    """ids must be a permutation of [0, N). An id >= N is never used as an index (the
+    Gaussian is dropped: no out-of-bounds write) and the next call returns PTGS_EINVAL."""
+    from pathtracer_gaussiansplatting_amd import Renderer, PtgsError
+    from pathtracer_gaussiansplatting_amd._abi import PTGS_EINVAL
+    W, H, n = 160, 96, 2000
+    g = Y.gaussians_c2(n, seed=47)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    r = Renderer(0)
+    try:
+        dg = {k: _dev(v) for k, v in g.items()}
+        good = torch.arange(n, dtype=torch.int32, device="cuda")
+        bad = good.clone()
+        bad[17] = n + 5
+        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        r.splat_gaussians(dict(dg, ids=bad), ubo, W, H, out)
+        torch.cuda.synchronize()
+        with pytest.raises(PtgsError) as ei:
+            r.splat_gaussians(dict(dg, ids=good), ubo, W, H, out)
+        assert ei.value.code == PTGS_EINVAL
+        r.splat_gaussians(dict(dg, ids=good), ubo, W, H, out)
+        torch.cuda.synchronize()
+        ref = oracle_lib.splat_gaussians(g, ubo, W, H)
+        assert U.rel_l2(out.cpu().numpy(), ref["image"]) < 1e-4
+    finally:
+        r.close()
