@@ -292,6 +292,29 @@ def main():
             out["pt_wavefront"] = {"value": round(sum_over_ranks(float(wst.extension_rays + wst.shadow_rays)) / wdt / 1e6,
                                                   3), "unit": "Mrays/s", "ms_per_step": round(wdt / args.steps * 1e3, 3),
                                    "note": "same C3 frames through the wavefront stages (PTGS_FLAG_PT_WAVEFRONT)"}
+        # the viewer's protocol (recordCommandBuffer, engine.cpp:1971-1976): one sample per call at the
+        # swapchain size, running mean of raygen_camera.rgen:80-87 into the accumulator, frame_count
+        # advancing per call - SPP consecutive 1-spp calls against the one SPP-sample launch above
+        if world == 1:
+            vacc = torch.zeros_like(accum)
+            for k in range(4):
+                r.trace_camera(make_ubo(pose, scene, k, ambient=(0.3, 0.4, 0.5, 1.0), height=H), W, H, vacc, spp=1,
+                               stream=stream)
+            vubos = [make_ubo(pose, scene, k, ambient=(0.3, 0.4, 0.5, 1.0), height=H) for k in range(SPP)]
+            torch.cuda.synchronize()
+            r.stats_reset(stream)
+            t0 = time.perf_counter()
+            for u in vubos:
+                r.trace_camera(u, W, H, vacc, spp=1, stream=stream)
+            torch.cuda.synchronize()
+            vdt = time.perf_counter() - t0
+            vst = r.stats()
+            vm = (vst.extension_rays + vst.shadow_rays) / vdt / 1e6
+            out["viewer_1spp"] = {"value": round(vm, 3), "unit": "Mrays/s", "ms_per_call": round(vdt / SPP * 1e3, 4),
+                                  "calls": SPP, "vs_launch": round(vm / mrays, 4),
+                                  "workload": f"C3, {SPP} consecutive ptgs_trace_camera(spp=1) calls at {W}x{H} "
+                                              "(the viewer's per-frame call; running mean)"}
+            del vacc
         # the GPU BVH builders on the same scene: build time and one traced frame each. PTGS_FLAG_GPU_BVH
         # is the host's binned SAH run on the GPU (the same tree: the same traversal cost);
         # PTGS_FLAG_GPU_LBVH the linear BVH (fastest rebuilds, weaker tree)

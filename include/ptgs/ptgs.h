@@ -281,6 +281,10 @@ int ptgs_trace_camera_rows(ptgs_ctx* ctx, const ptgs_ubo* ubo, uint32_t width, u
  * float[W*H]. */
 int ptgs_trace_depth(ptgs_ctx* ctx, const ptgs_ubo* ubo, uint32_t width, uint32_t height, float* depth,
                      void* hip_stream);
+/* The same for pixel rows [row_begin, row_end) only (the tile-row shard of the hybrid frame: each rank
+ * traces the depth of its own rows); the other rows of depth are left untouched. */
+int ptgs_trace_depth_rows(ptgs_ctx* ctx, const ptgs_ubo* ubo, uint32_t width, uint32_t height, uint32_t row_begin,
+                          uint32_t row_end, float* depth, void* hip_stream);
 
 /* Toroidal data-collection tracer (shaders/rt_datacollect/raygen.rgen:31-141): one ray per
  * RaySample (device array, n entries), launch grid side x side with side = ceil(sqrt(n))
@@ -348,6 +352,11 @@ typedef struct ptgs_gaussians {
      * a Gaussian whose id is >= N is dropped (never written out of bounds) and the next splat call
      * returns PTGS_EINVAL; duplicate ids are not detected (their keys collide: undefined order) */
     const uint32_t* ids;
+    /* NULL, or per chunk of 256 consecutive Gaussians (ptgs_gaussians_chunk_bounds, 8 floats each): a
+     * frame restricted to tile rows skips whole chunks whose conservative screen bound misses them,
+     * before loading any of their Gaussians (the tile-row shard of several GPUs: each rank preprocesses
+     * the chunks that reach its rows instead of all N). Outputs are unchanged. */
+    const float* chunk_bounds;
 } ptgs_gaussians;
 
 typedef struct ptgs_splat_stats {
@@ -408,6 +417,12 @@ int ptgs_splat_gaussians_views(ptgs_ctx* ctx, const ptgs_gaussians* g, uint32_t 
  * (like ptgs_scene_upload's BVH build): synchronises; device temporaries are freed. */
 int ptgs_gaussians_sort_spatial(ptgs_ctx* ctx, const ptgs_gaussians* g, float* means, float* scales, float* rotations,
                                 float* opacities, float* colors, uint32_t* ids, void* hip_stream);
+
+/* Bounds of every chunk of 256 consecutive Gaussians of g (device float[8 * ceil(count / 256)]): the
+ * box of its means (min x, y, z, then max x, y, z at [4..6]) and its largest scale ([3]); [7] = 0. For
+ * ptgs_gaussians.chunk_bounds; useful when chunks are spatially compact (ptgs_gaussians_sort_spatial's
+ * order). Recompute after the Gaussians change. Stream-ordered. */
+int ptgs_gaussians_chunk_bounds(ptgs_ctx* ctx, const ptgs_gaussians* g, float* bounds, void* hip_stream);
 
 /* Report of the stream-ordered splat (no stats): waits for hip_stream and the context's view streams,
  * then returns (and clears) the counts since the last query. frames / views[v]: frames left

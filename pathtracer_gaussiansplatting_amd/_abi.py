@@ -139,7 +139,8 @@ class TraceStats(C.Structure):
 
 class Gaussians(C.Structure):
     _fields_ = [("means", C.c_void_p), ("scales", C.c_void_p), ("rotations", C.c_void_p),
-                ("opacities", C.c_void_p), ("colors", C.c_void_p), ("count", C.c_uint32), ("ids", C.c_void_p)]
+                ("opacities", C.c_void_p), ("colors", C.c_void_p), ("count", C.c_uint32), ("ids", C.c_void_p),
+                ("chunk_bounds", C.c_void_p)]
 
 
 class SplatStats(C.Structure):
@@ -203,6 +204,8 @@ SYMBOLS = {
     "ptgs_splat_status_read": (_I, [_P, C.POINTER(SplatStatus), _P]),
     "ptgs_splat_reserve": (_I, [_P, _U]),
     "ptgs_gaussians_sort_spatial": (_I, [_P, C.POINTER(Gaussians), _P, _P, _P, _P, _P, _P, _P]),
+    "ptgs_gaussians_chunk_bounds": (_I, [_P, C.POINTER(Gaussians), _P, _P]),
+    "ptgs_trace_depth_rows": (_I, [_P, C.POINTER(Ubo), _U, _U, _U, _U, _P, _P]),
     "ptgs_knn3_mean_dist2": (_I, [_P, _P, _U, _P, _P]),
     "ptgs_gaussians_from_points": (_I, [_P, _P, _P, _U, _P, _P, _P, _P, _P, _P]),
     "ptgs_comm_unique_id": (_I, [_P]),

@@ -509,6 +509,11 @@ int ptgs_trace_camera(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_t h, 
 }
 
 int ptgs_trace_depth(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_t h, float* depth, void* stream) {
+  return ptgs_trace_depth_rows(c, ubo, w, h, 0, h, depth, stream);
+}
+
+int ptgs_trace_depth_rows(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_t h, uint32_t row_begin,
+                          uint32_t row_end, float* depth, void* stream) {
   if (!c || !ubo || !depth) return fail(c, PTGS_EINVAL, "null argument");
   if (!c->has_scene) return fail(c, PTGS_ENOSCENE, "no scene uploaded");
   if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
@@ -519,7 +524,7 @@ int ptgs_trace_depth(ptgs_ctx* c, const ptgs_ubo* ubo, uint32_t w, uint32_t h, f
   if (rc) return rc;
   ViewMat vm;
   std::memcpy(vm.m, ubo->view, sizeof(vm.m));
-  hipError_t e = launch_pt_depth(c->dsc, cp, vm, depth, w, h, ubo->frame_count, (hipStream_t)stream);
+  hipError_t e = launch_pt_depth(c->dsc, cp, vm, depth, w, h, row_begin, row_end, ubo->frame_count, (hipStream_t)stream);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "pt_depth launch: %s", hipGetErrorString(e));
   return PTGS_OK;
 }
@@ -720,6 +725,16 @@ int ptgs_gaussians_sort_spatial(ptgs_ctx* c, const ptgs_gaussians* g, float* mea
   HIPCHK(c, hipSetDevice(c->device));
   const hipError_t e = splat_sort_spatial(g, means, scales, rotations, opacities, colors, ids, (hipStream_t)stream);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "ptgs_gaussians_sort_spatial: %s", hipGetErrorString(e));
+  return PTGS_OK;
+}
+
+int ptgs_gaussians_chunk_bounds(ptgs_ctx* c, const ptgs_gaussians* g, float* bounds, void* stream) {
+  if (!c || !g || !bounds) return fail(c, PTGS_EINVAL, "null argument");
+  if (g->count && (!is_device_ptr(g->means) || !is_device_ptr(g->scales) || !is_device_ptr(bounds)))
+    return fail(c, PTGS_EINVAL, "means / scales / bounds must be device pointers");
+  HIPCHK(c, hipSetDevice(c->device));
+  const hipError_t e = splat_chunk_bounds(g, bounds, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, PTGS_EHIP, "ptgs_gaussians_chunk_bounds: %s", hipGetErrorString(e));
   return PTGS_OK;
 }
 

@@ -344,13 +344,14 @@ __global__ __launch_bounds__(256, TEX ? 1 : PTGS_TORUS_MIN_WAVES) void pt_torus_
 // view-space distance -(view * hit).z of the hit point, +inf on a miss. One work-item per pixel.
 template <bool TEX>
 __global__ __launch_bounds__(256) void pt_depth_kernel(DevScene sc, CamParams cp, ViewMat vm, float* __restrict__ depth,
-                                                       uint32_t W, uint32_t H, uint32_t frame) {
+                                                       uint32_t W, uint32_t H, uint32_t row0, uint32_t row1,
+                                                       uint32_t frame) {
   const uint32_t lid = threadIdx.x;
   const uint32_t wave = lid >> 6, lane = lid & 63u;
   const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-  const uint32_t y = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+  const uint32_t y = row0 + blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
   __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
-  if (x >= W || y >= H) return;
+  if (x >= W || y >= row1) return;
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
   const uint32_t seed = y * W + x + frame * 719393u;
   const float ux = ((float)x + 0.5f) / (float)W, uy = ((float)y + 0.5f) / (float)H;
@@ -435,9 +436,21 @@ hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accu
   // heavy tiles first once a launch of this grid has recorded its tile times; launches of fewer than
   // PTGS_PT_SCHED_MIN pixel-samples skip it (C1's 65k: the order kernel's launch would cost more than
   // the tail it saves)
+  if (ps && PTGS_PT_SCHED && ps->owned && ps->stream != stream) {
+    // another stream holds the schedule: take it over once that stream has drained (its launches may
+    // still read `order`), else this launch runs unscheduled and records nothing
+    if (hipStreamQuery(ps->stream) != hipErrorNotReady) {
+      ps->owned = false;
+      ps->gx = ps->gy = 0;  // (its recorded times belong to the old stream's grid: record afresh)
+    } else {
+      ps = nullptr;
+    }
+  }
   if (ps && PTGS_PT_SCHED && (uint64_t)W * (row1 - row0) * spp >= (uint64_t)PTGS_PT_SCHED_MIN) {
     const uint32_t n = grid.x * grid.y;
     hipError_t e;
+    ps->stream = stream;
+    ps->owned = true;
     if (n > ps->cap) {
       free_pt_sched(*ps);
       if ((e = hipMalloc(&ps->cost, (size_t)n * 4)) || (e = hipMalloc(&ps->order, (size_t)n * 4))) return e;
@@ -463,10 +476,12 @@ hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accu
 }
 
 hipError_t launch_pt_depth(const DevScene& sc, const CamParams& cp, const ViewMat& vm, float* depth, uint32_t W,
-                           uint32_t H, uint32_t frame, hipStream_t stream) {
-  dim3 grid((W + 15u) / 16u, (H + 15u) / 16u);
+                           uint32_t H, uint32_t row0, uint32_t row1, uint32_t frame, hipStream_t stream) {
+  row1 = row1 < H ? row1 : H;
+  if (row1 <= row0) return hipSuccess;
+  dim3 grid((W + 15u) / 16u, (row1 - row0 + 15u) / 16u);
   auto k = sc.uses_textures ? pt_depth_kernel<true> : pt_depth_kernel<false>;
-  hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, sc, cp, vm, depth, W, H, frame);
+  hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, sc, cp, vm, depth, W, H, row0, row1, frame);
   return hipGetLastError();
 }
 

@@ -17,14 +17,18 @@ struct ViewMat {  // ubo.view (column-major)
 };
 
 hipError_t launch_pt_depth(const DevScene& sc, const CamParams& cp, const ViewMat& vm, float* depth, uint32_t W,
-                           uint32_t H, uint32_t frame, hipStream_t stream);
+                           uint32_t H, uint32_t row0, uint32_t row1, uint32_t frame, hipStream_t stream);
 
 // The megakernel's tile schedule: per-tile times of the last launch and the order built from them
-// (tiles that took longest first); owned by the context, valid for the grid (gx, gy) it was recorded on
+// (tiles that took longest first); owned by the context, valid for the grid (gx, gy) it was recorded
+// on and used only by launches on the stream that recorded it (another stream's order kernel could
+// rewrite `order` while a launch reads it); the schedule moves to a new stream once the old one is idle
 struct PtSched {
   uint32_t* cost = nullptr;
   uint32_t* order = nullptr;
   uint32_t cap = 0, gx = 0, gy = 0;
+  hipStream_t stream = nullptr;
+  bool owned = false;  // `stream` holds the schedule
 };
 void free_pt_sched(PtSched& ps);
 

@@ -23,6 +23,8 @@ hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
 // 3D Morton order of the means: a reordered copy + the original indices (synchronises s)
 hipError_t splat_sort_spatial(const ptgs_gaussians* g, float* means, float* scales, float* rots, float* opac,
                               float* colors, uint32_t* ids, hipStream_t s);
+// per 256-Gaussian chunk: box of the means + largest scale (8 floats; stream-ordered)
+hipError_t splat_chunk_bounds(const ptgs_gaussians* g, float* bounds, hipStream_t s);
 // grow the pair buffers and the spill pool to at least `pairs` (frees / reallocates: waits for the device)
 hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs);
 struct SplatStatusOut {

@@ -47,6 +47,7 @@ struct SplatCam {
   uint32_t W, H;
   uint32_t grid_x, grid_y;
   uint32_t row_begin, row_end;  // tile rows
+  uint32_t cull;                // tile rows restricted and chunk bounds given: PreArgs.cskip is valid
 };
 
 struct DevBuf {
@@ -60,6 +61,8 @@ struct SplatWorkspace {
   DevBuf cursor, fz, pub_offs, keys_pub, vals_pub;  // fused front end (see gs_bin_fused_kernel); fz: counters
   DevBuf dbg_depths, fzp, nzbuf, order;  // order: the blend's tile order (heavy first, fused frames)
   DevBuf crect, sp_keys, sp_vals;  // spilled tiles (gs_spill_tile): chunk rects, the spill pool
+  DevBuf fsq;                 // the fused front end's slice queue
+  DevBuf cskip;               // per 256-Gaussian chunk: skipped by a tile-row-restricted frame
   uint32_t sp_cap = 0;        // spill pool capacity (pairs)
   uint32_t incomplete = 0;    // frames reported incomplete (spill pool exhausted) since the last status clear
   uint32_t spilled_base = 0, incomplete_base = 0;  // device counters fz[9] / fz[10] at the last status clear
@@ -89,7 +92,7 @@ void splat_workspace_destroy(SplatWorkspace* w) {
                    &w->vals_out, &w->ranges, &w->hist, &w->tile_info, &w->group_total, &w->tile_slots, &w->point_keys,
                    &w->total, &w->rect, &w->large, &w->large_ctr, &w->sort_scratch, &w->cursor, &w->fz,
                    &w->pub_offs, &w->keys_pub, &w->vals_pub, &w->dbg_depths, &w->fzp, &w->nzbuf, &w->order,
-                   &w->crect, &w->sp_keys, &w->sp_vals};
+                   &w->crect, &w->sp_keys, &w->sp_vals, &w->fsq, &w->cskip};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
@@ -133,6 +136,7 @@ struct PreArgs {
   const uint32_t* ids;  // caller's index of Gaussian i (NULL: i): keys, values, records and the
                         // per-Gaussian outputs use it, so a reordered set renders like the original
   uint32_t* bad_ids;    // pinned host word set to 1 when an id is >= n (the Gaussian is dropped)
+  const uint8_t* cskip;  // per 256-Gaussian chunk: 1 = its bound misses the frame's rows (gs_chunk_cull_kernel)
 };
 
 // Stores that may stream past L2 (A/B: GS_NT_REC for the blend records, GS_NT_OUT for the image)
@@ -291,6 +295,74 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   gs_st4<GS_NT_REC>(rec + 3 * o + 1, make_float4(-0.5f * con.z * L2E, __log2f(con.w), cr, cg));
   gs_st4<GS_NT_REC>(rec + 3 * o + 2, make_float4(cbl, ex, ey, d));
   return rect;
+}
+
+// Can any Gaussian of a chunk touch a tile of the frame's rows (cam.row_begin, row_end) and columns?
+// Conservative, from the chunk's bounds (box of the means, largest scale): view depths over the box's
+// corners are exact (linear); every mean projects inside the hull of the corners' projections when all
+// of them lie in front of the camera; and a Gaussian's 3-sigma radius is at most
+// 3 sqrt(|J|_F^2 |W|_F^2 s_max^2 + 0.3 + sqrt(0.1)) + 1 px with |J|_F^2 <= (fx^2 (1 + (1.3 tan_x)^2)
+// + fy^2 (1 + (1.3 tan_y)^2)) / d_min^2 (the EWA Jacobian at the clamped point, gs_preprocess_one).
+// Margins of 1 % and a tile on every side absorb the rounding. Returns true when the chunk is sure to
+// contribute nothing: every mean within the near plane (d <= 0.2), or its bound misses the rows /
+// columns. Unbounded cases (a corner close to the camera, non-finite bounds) return false.
+__device__ __forceinline__ bool gs_chunk_misses(const SplatCam& cam, const float4 lo, const float4 hi) {
+  if (!(isfinite(lo.x) && isfinite(lo.y) && isfinite(lo.z) && isfinite(hi.x) && isfinite(hi.y) && isfinite(hi.z) &&
+        isfinite(lo.w)))
+    return false;
+  float dmin = INFINITY, dmax = -INFINITY, xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
+  bool front = true;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float x = (k & 1) ? hi.x : lo.x, y = (k & 2) ? hi.y : lo.y, z = (k & 4) ? hi.z : lo.z;
+    const v4 pv = mv4(cam.view, x, y, z, 1.0f);
+    const v4 ph = mv4(cam.mvp, x, y, z, 1.0f);
+    const float d = -pv.z;
+    dmin = fminf(dmin, d);
+    dmax = fmaxf(dmax, d);
+    front = front && ph.w > 0.1f;
+    const float iw = 1.0f / ph.w;
+    const float sx = ndc2pix(ph.x * iw, (int)cam.W), sy = ndc2pix(ph.y * iw, (int)cam.H);
+    xmin = fminf(xmin, sx);
+    xmax = fmaxf(xmax, sx);
+    ymin = fminf(ymin, sy);
+    ymax = fmaxf(ymax, sy);
+  }
+  if (dmax < 0.19f) return true;                // every Gaussian is culled by the near test
+  if (dmin < 0.25f || !front) return false;     // too close to bound the projection
+  const float *V = cam.view;
+  const float wf2 = ((V[0] * V[0] + V[1] * V[1]) + V[2] * V[2]) + ((V[4] * V[4] + V[5] * V[5]) + V[6] * V[6]) +
+                    ((V[8] * V[8] + V[9] * V[9]) + V[10] * V[10]);
+  const float tx = 1.3f * cam.tan_fovx, ty = 1.3f * cam.tan_fovy;
+  const float jf2 = (cam.fx * cam.fx * (1.0f + tx * tx) + cam.fy * cam.fy * (1.0f + ty * ty)) / (dmin * dmin);
+  const float lam = jf2 * wf2 * lo.w * lo.w;
+  const float R = 3.0f * sqrtf(1.01f * (lam + 0.62f)) + 3.0f;  // px
+  if (!isfinite(R)) return false;
+  const float t = (float)GS_BLOCK_Y;
+  const float r0 = floorf((ymin - R) / t) - 1.0f, r1 = floorf((ymax + R + t) / t) + 1.0f;  // rows [r0, r1]
+  const float c0 = floorf((xmin - R) / t) - 1.0f, c1 = floorf((xmax + R + t) / t) + 1.0f;
+  return r1 < (float)cam.row_begin || r0 >= (float)cam.row_end || c1 < 0.0f || c0 >= (float)cam.grid_x;
+}
+
+// The stores a Gaussian of a skipped chunk owes: the empty rect (the scatter and gs_spill_tile read
+// it) and, on a published frame, zero radius / tiles touched
+__device__ __forceinline__ void gs_store_skipped(const PreArgs& A, uint32_t i) {
+  if (A.rects) A.rects[i] = make_ushort4(0, 0, 0, 0);
+  if (A.radii) {
+    const uint32_t o = A.ids ? A.ids[i] : i;
+    if (o < A.n) {
+      A.radii[o] = 0;
+      A.touched[o] = 0;
+    }
+  }
+}
+
+// One flag per 256-Gaussian chunk for a tile-row-restricted frame (its own small launch, so that the
+// front-end kernels keep no bound arithmetic: they read the flag before loading a chunk)
+__global__ __launch_bounds__(256) void gs_chunk_cull_kernel(SplatCam cam, const float4* __restrict__ cb, uint32_t nch,
+                                                            uint8_t* __restrict__ skip) {
+  const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+  if (c < nch) skip[c] = gs_chunk_misses(cam, cb[2 * c], cb[2 * c + 1]) ? 1 : 0;
 }
 
 // ---- binning --------------------------------------------------------------------------------------
@@ -480,8 +552,7 @@ __device__ __forceinline__ void gs_spill_rearm(uint32_t* fz, uint32_t* k_host) {
   const uint32_t d = fz[8];
   __atomic_store_n(k_host + 8, d, __ATOMIC_RELAXED);
   if (d > fz[11]) fz[11] = d;
-  fz[8] = 0;
-  __threadfence_system();
+  fz[8] = 0;  // (k_host[8] reaches the host with the blend's system fence: no fence here)
 }
 
 // Bounding tile rect (x0, y0, x1, y1) of one front-end workgroup's clipped Gaussian rects, reduced over
@@ -547,7 +618,11 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
   for (uint32_t base = b0 + wave * 64u; base < b1; base += GS_COUNT_THREADS) {
     const uint32_t i = base + lane;
     ushort4 rc = make_ushort4(0, 0, 0, 0);
-    if (i < b1) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i) : gs_preprocess_one<false>(cam, A, i);
+    // (tile-row shard with chunk bounds: a 256-Gaussian chunk whose bound misses the rows is skipped
+    // before its Gaussians are loaded; a wave's 64 lie in at most two chunks)
+    const bool skip = cam.cull && i < b1 && A.cskip[i >> 8];
+    if (i < b1 && !skip) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i) : gs_preprocess_one<false>(cam, A, i);
+    else if (i < b1 && blockIdx.x == 0) gs_store_skipped(A, i);
     uint32_t xw, yh;
     gs_clip(rc, ty0, ty1, xw, yh);
     if (yh) {
@@ -780,6 +855,8 @@ struct GsFused {  // the sort's and the blend's view of a fused-front-end frame 
   uint32_t* fzp;      // per front-end workgroup: (pairs, reservations)
   uint32_t nwg;
   const uint32_t* order;  // blend workgroup -> tile (heavy tiles first; null: row-major)
+  uint2* fsq;             // the front end's slice queue (re-armed by block (0, 0): entries and fz[12..14])
+  uint32_t fsq_cap;
 };
 // GS_STAMP builds (tools/gs_stamps.py): per-workgroup s_memrealtime (100 MHz) stamps at phase
 // boundaries of the fused front end and the blend, read back with ptgs_debug_stamps.
@@ -802,65 +879,32 @@ __device__ unsigned long long g_gs_stamps[2][GS_STAMP_WG * GS_STAMP_N];
 #define GS_FUSED_WG 512  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
 #endif
 
-// Workgroup-cooperative pair walk of the fused front end: the chunk's rects (s_e: x0 | w << 16,
-// y0 | h << 16, key index, depth bits) and the inclusive scan of their areas (s_incl) are in LDS;
-// work-item t takes the contiguous pairs [t q, t q + q) of the chunk's P (q = ceil(P / GS_FUSED_WG)):
-// one binary search for its first pair, then it steps through the rects (a heavy Gaussian's pairs are
-// spread over the whole workgroup instead of one wave). f(key index, x, y, depth bits).
-template <typename F>
-__device__ __forceinline__ void gs_wg_walk(const uint32_t* s_incl, const uint4* s_e, uint32_t ng, uint32_t P, F f) {
-  const uint32_t q = (P + GS_FUSED_WG - 1) / GS_FUSED_WG;
-  uint32_t p = threadIdx.x * q;
-  const uint32_t p1 = min(P, p + q);
-  if (p >= p1) return;
-  uint32_t lo = 0, hi = ng - 1;  // first j with incl[j] > p
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (s_incl[mid] > p) hi = mid;
-    else lo = mid + 1;
-  }
-  uint32_t j = lo;
-  uint4 e = s_e[j];
-  uint32_t w = e.x >> 16, r = p - (s_incl[j] - w * (e.y >> 16));
-  uint32_t ry = r / w, rx = r - ry * w;
-  for (;;) {
-    f(e.z, (e.x & 0xFFFFu) + rx, (e.y & 0xFFFFu) + ry, e.w);
-    if (++p >= p1) break;
-    if (++rx == w) {
-      rx = 0;
-      if (++ry == (e.y >> 16)) {  // next rect with pairs
-        do {
-          e = s_e[++j];
-        } while ((e.y >> 16) == 0u || (e.x >> 16) == 0u);
-        w = e.x >> 16;
-        ry = 0;
-      }
-    }
-  }
-}
-
-// The count walk of a chunk with at most GS_FUSED_QREG pairs per work-item: the same walk as
-// gs_wg_walk, with returning LDS atomics whose results (the pair's rank among the chunk's pairs of its
-// tile) are kept in registers with the pair, packed as k | rank << 13 | j << 21 (k: tile in the
-// chunk's rect, < 8192 = GS_BAND_TILES; rank < 256: one pair per Gaussian and tile; j: Gaussian in the
-// chunk, < 256). The scatter then writes each kept pair at its run's base + rank without walking the
-// rects again or touching an LDS atomic. Returns the work-item's pair count.
+// The count walk of one slice [p0, p1) of a chunk's pairs (at most GS_FUSED_QREG per work-item): the
+// chunk's rects (s_e: x0 | w << 16, y0 | h << 16, key index, depth bits) and the inclusive scan of
+// their areas (s_incl) are in LDS; work-item t takes the contiguous pairs [p0 + t q, p0 + t q + q)
+// (q = ceil((p1 - p0) / GS_FUSED_WG)): one binary search for its first pair, then it steps through the
+// rects (a heavy Gaussian's pairs are spread over the whole workgroup instead of one wave). Returning
+// LDS atomics give each pair its rank among the slice's pairs of its tile, kept in registers with the
+// pair, packed as k | rank << 13 | j << 21 (k: tile in the chunk's rect, < 8192 = GS_BAND_TILES; rank
+// < 256: one pair per Gaussian and tile; j: Gaussian in the chunk, < 256). The scatter then writes each
+// kept pair at its run's base + rank without walking the rects again or touching an LDS atomic.
+// Returns the work-item's pair count.
 #ifndef GS_FUSED_QREG
-#define GS_FUSED_QREG 16  // (C2 needs <= 7; 8 and 16 measured equal: 50 / 53 VGPRs)
+#define GS_FUSED_QREG 8  // pairs per work-item of a slice (GS_FUSED_SLICE / GS_FUSED_WG; C2 needs <= 7)
 #endif
 #ifndef GS_FUSED_KEEP
 #define GS_FUSED_KEEP 1
 #endif
 #define GS_KEEP_RB (GS_FUSED_THREADS <= 256 ? 8u : 9u)  // bits of rank and of j (< GS_FUSED_THREADS)
 static_assert(GS_FUSED_THREADS <= 512 && GS_BAND_TILES <= 8192, "gs_wg_count_keep's packing");
-__device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, const uint4* s_e, uint32_t ng, uint32_t P,
-                                                     uint32_t* s_hist, uint32_t bx0, uint32_t by0, uint32_t rw,
-                                                     uint32_t (&pk)[GS_FUSED_QREG]) {
-  const uint32_t q = (P + GS_FUSED_WG - 1) / GS_FUSED_WG;
-  uint32_t p = threadIdx.x * q;
-  const uint32_t p1 = min(P, p + q);
-  if (p >= p1) return 0;
-  const uint32_t cnt = p1 - p;
+__device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, const uint4* s_e, uint32_t ng, uint32_t p0,
+                                                     uint32_t p1, uint32_t* s_hist, uint32_t bx0, uint32_t by0,
+                                                     uint32_t rw, uint32_t (&pk)[GS_FUSED_QREG]) {
+  const uint32_t q = (p1 - p0 + GS_FUSED_WG - 1) / GS_FUSED_WG;
+  uint32_t p = p0 + threadIdx.x * q;
+  const uint32_t pe = min(p1, p + q);
+  if (p >= pe) return 0;
+  const uint32_t cnt = pe - p;
   uint32_t lo = 0, hi = ng - 1;  // first j with incl[j] > p
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -892,7 +936,31 @@ __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, con
   return cnt;
 }
 
-__global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
+// Load balance. A chunk's pairs are walked in slices of at most GS_FUSED_SLICE pairs. The owner (the
+// chunk's workgroup) walks slice 0 and publishes the others to a queue (fsq, entries (owner + 1, j));
+// helper workgroups (the rows after the owners) claim queued slices, rebuild the chunk's rects (the
+// same preprocess, no stores) and walk them: every (slice, tile) run reserves its own range, so a
+// chunk that holds many times the mean pairs (Gaussians close to a moving camera) no longer sets the
+// kernel's length alone. After its slice 0 an owner claims its own still-queued slices (it never
+// waits), so no slice depends on a helper: a helper waits only for owners that have not published yet
+// (owners precede helpers in dispatch order), and gives up after ~100 us (a slice it would have taken
+// is then its owner's). Queue words: fz[GS_FSQ_W] claims (helpers), fz[GS_FSQ_W + 1] entries,
+// fz[GS_FSQ_W + 2] owners done;
+// entries are 0 (not written), owner + 1 (open), GS_FSQ_TAKEN; the blend's block (0, 0) re-arms them.
+#ifndef GS_FUSED_SLICE
+#define GS_FUSED_SLICE 4096u  // pairs per slice (C2's chunks hold 1.6k on average, 3.3k at most: one slice)
+#endif
+#ifndef GS_FUSED_HELPERS
+#define GS_FUSED_HELPERS 128u  // helper workgroups per band (one queued slice each)
+#endif
+#define GS_FSQ_TAKEN 0xFFFFFFFFu
+#define GS_FSQ_W 32  // the queue words' offset in fz: a cache line of their own (helpers poll them)
+#ifndef GS_FUSED_WAVES
+#define GS_FUSED_WAVES 6  // waves per SIMD (3 workgroups of 512 work-items per CU; 8 forces SGPR spills)
+#endif
+static_assert(GS_FUSED_SLICE <= (uint32_t)GS_FUSED_WG * GS_FUSED_QREG, "a slice's pairs are kept in registers");
+
+__global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                          uint32_t scap,
                                                                          uint32_t* __restrict__ cursor,
                                                                          uint32_t* __restrict__ fz,
@@ -904,139 +972,260 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
                                                                          ushort4* __restrict__ crect,
                                                                          ushort4* __restrict__ rects_out,
                                                                          float* __restrict__ depths_out,
-                                                                         uint32_t* k_host) {
+                                                                         uint32_t* k_host, uint2* __restrict__ fsq,
+                                                                         uint32_t fsq_cap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // <= band_rows * grid_x
   __shared__ uint32_t s_red[4][GS_FUSED_WG / 64];
   __shared__ uint32_t s_tot[GS_FUSED_WG / 64];
   __shared__ uint32_t s_incl[GS_FUSED_THREADS];
   __shared__ uint4 s_e[GS_FUSED_THREADS];
+  __shared__ uint32_t s_job[4];  // helpers: (owner, slice) claimed; owners: queue base of their slices
   static_assert(GS_FUSED_THREADS >= GS_ORDER_BUCKETS, "gs_tile_order's buckets live in s_incl");
   if (order && blockIdx.y == gridDim.y - 1) {  // the extra row of blocks: the blend's tile order
     if (blockIdx.x == 0) gs_tile_order(prev_ranges, order, order_tb, order_te, s_incl);
     return;
   }
   STAMP(0, 0);
-  uint32_t ty0, ty1;
-  gs_band(bg, ty0, ty1);
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint32_t i = blockIdx.y * bg.chunk + threadIdx.x;  // chunk <= GS_FUSED_THREADS (host)
-  const bool own = threadIdx.x < bg.chunk && i < A.n;
-  ushort4 rc = make_ushort4(0, 0, 0, 0);
-  const uint32_t o = own && A.ids ? A.ids[i] : i;  // the key's index (the caller's)
-  float d = 0.0f;  // view depth (every band's blocks need it for the keys; only band 0 stores it)
-  if (own) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
-  if (own && blockIdx.x == 0) {  // for gs_spill_tile: the rect (empty: culled) and depth in walk order
-    rects_out[i] = rc;
-    depths_out[i] = d;
-  }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) gs_spill_rearm(fz, k_host);
-#ifdef GS_STAMP
-  if (threadIdx.x == 0) __builtin_amdgcn_s_waitcnt(0);  // (wave 0's preprocess, loads included)
-  STAMP(0, 6);
-#endif
-  uint32_t xw, yh;
-  gs_clip(rc, ty0, ty1, xw, yh);
-  // the chunk's bounding tile rect (within the band): the LDS histogram covers only it, so zeroing
-  // and the reservation scan touch ~100 entries for a spatially coherent chunk instead of the band's
-  uint32_t bx0 = 0xFFFFu, by0 = 0xFFFFu, bx1 = 0u, by1 = 0u;
-  if (yh) {
-    bx0 = xw & 0xFFFFu;
-    bx1 = bx0 + (xw >> 16);
-    by0 = yh & 0xFFFFu;
-    by1 = by0 + (yh >> 16);
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    bx0 = min(bx0, (uint32_t)__shfl_xor((int)bx0, off));
-    by0 = min(by0, (uint32_t)__shfl_xor((int)by0, off));
-    bx1 = max(bx1, (uint32_t)__shfl_xor((int)bx1, off));
-    by1 = max(by1, (uint32_t)__shfl_xor((int)by1, off));
-  }
-  // the rects and the inclusive scan of their areas for the workgroup walk: the per-wave partials of
-  // both (rect bounds, area totals) meet behind one barrier
-  const uint32_t area = yh ? (xw >> 16) * (yh >> 16) : 0u;
-  const uint32_t incl = wave_incl_scan(area);
-  if (lane == 0) {
-    s_red[0][wave] = bx0;
-    s_red[1][wave] = by0;
-    s_red[2][wave] = bx1;
-    s_red[3][wave] = by1;
-  }
-  if (lane == 63) s_tot[wave] = incl;
-  if (threadIdx.x < GS_FUSED_THREADS) s_e[threadIdx.x] = make_uint4(xw, yh, o, __float_as_uint(d));
-  __syncthreads();
-  STAMP(0, 7);
-  uint32_t run = incl, P = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < GS_FUSED_WG / 64; ++w) {
-    bx0 = min(bx0, s_red[0][w]);
-    by0 = min(by0, s_red[1][w]);
-    bx1 = max(bx1, s_red[2][w]);
-    by1 = max(by1, s_red[3][w]);
-    const uint32_t tw = s_tot[w];
-    run += w < wave ? tw : 0u;
-    P += tw;
-  }
-  if (threadIdx.x < GS_FUSED_THREADS) s_incl[threadIdx.x] = run;
-  const uint32_t rw = bx1 > bx0 ? bx1 - bx0 : 0u, rh = by1 > by0 ? by1 - by0 : 0u, nt = rw * rh;
-  if (threadIdx.x == 0)  // the workgroup's bounding rect (gs_spill_tile; empty: x0 > x1)
-    crect[blockIdx.y * gridDim.x + blockIdx.x] =
-        nt ? make_ushort4((unsigned short)bx0, (unsigned short)by0, (unsigned short)bx1, (unsigned short)by1)
-           : make_ushort4(1, 1, 0, 0);
-  for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_WG) s_hist[k] = 0;
-  __syncthreads();  // (the scan and the zeroed histogram)
-  STAMP(0, 1);
-  STAMP_SYNC();
-  STAMP(0, 2);
-  // (uniform) pairs kept in registers between the count and the scatter, or a second walk
-  const bool keep = GS_FUSED_KEEP && P <= (uint32_t)GS_FUSED_WG * GS_FUSED_QREG;
-  uint32_t pk[GS_FUSED_QREG];
-  uint32_t kept = 0;
-  if (keep) {
-    kept = gs_wg_count_keep(s_incl, s_e, GS_FUSED_THREADS, P, s_hist, bx0, by0, rw, pk);
-  } else {
-    gs_wg_walk(s_incl, s_e, GS_FUSED_THREADS, P, [&](uint32_t, uint32_t x, uint32_t y, uint32_t) {
-      atomicAdd(s_hist + (y - by0) * rw + (x - bx0), 1u);
-    });
-  }
-  __syncthreads();
-  STAMP(0, 3);
-  // reserve: one returning atomic per touched tile (all of a work-item's issued before any is used);
-  // the LDS entry becomes the run's base
-  uint32_t pairs = 0, res = 0;
-  const float rcp_rw = 1.0f / (float)max(rw, 1u);
-  for (uint32_t k0 = threadIdx.x; k0 < nt; k0 += 4 * GS_FUSED_WG) {
-    uint32_t c[4], t[4], base[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t k = k0 + j * GS_FUSED_WG;
-      c[j] = k < nt ? s_hist[k] : 0u;
-      uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13 * 2^13: exact after the fix-ups
-      ry = ry * rw > k ? ry - 1 : ry;
-      ry = (ry + 1) * rw <= k ? ry + 1 : ry;
-      t[j] = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
+  const uint32_t nown = bg.chunks * gridDim.x;  // owner workgroups
+  const bool owner = blockIdx.y < bg.chunks;
+  if (owner && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) gs_spill_rearm(fz, k_host);
+  uint32_t acc_pairs = 0, acc_res = 0;  // this workgroup's reservations over all its slices (per work-item)
+  uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;  // the owner whose chunk is processed
+  uint32_t slice = 0;
+  {  // helpers claim one queued slice (one per helper: no loop keeps the camera's registers live)
+    if (!owner) {
+      if (threadIdx.x == 0) {
+        uint32_t job = 0xFFFFFFFFu, hidx = 0, spins = 0;
+        for (;;) {
+          if (!hidx) hidx = atomicAdd(fz + GS_FSQ_W, 1u) + 1u;  // (1-based: 0 = none claimed)
+          const uint32_t idx = hidx - 1u;
+          if (idx >= fsq_cap) break;
+          // (the entry as one 64-bit word: owner + 1 and slice arrive together, no fence needed)
+          const unsigned long long ev = __hip_atomic_load(reinterpret_cast<unsigned long long*>(fsq + idx),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t v = (uint32_t)ev;
+          if (v == 0u) {  // not written yet: done when every owner has published and this index is past the end
+            const uint32_t done = __hip_atomic_load(fz + GS_FSQ_W + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t tail = __hip_atomic_load(fz + GS_FSQ_W + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((done >= nown && idx >= tail) || ++spins > 200u) break;
+            // (a few hundred helpers polling: every ~3 us, or their loads crowd out the owners' memory
+            // traffic; measured 3x slower owner phases at ~0.05 us per poll)
+            __builtin_amdgcn_s_sleep(127);
+            continue;
+          }
+          hidx = 0;  // this index is settled: the next iteration claims another
+          if (v != GS_FSQ_TAKEN && atomicCAS(&fsq[idx].x, v, GS_FSQ_TAKEN) == v) {
+            job = ((v - 1u) << 12) | (uint32_t)(ev >> 32);
+            break;
+          }
+        }
+        s_job[0] = job;
+      }
+      __syncthreads();
+      const uint32_t job = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_job[0]);
+      if (job == 0xFFFFFFFFu) {
+        if (threadIdx.x == 0) {
+          const uint32_t fw = blockIdx.y * gridDim.x + blockIdx.x;
+          fzp[2 * fw] = 0;
+          fzp[2 * fw + 1] = 0;
+        }
+        return;
+      }
+      wg = job >> 12;
+      slice = job & 0xFFFu;
     }
+    const uint32_t band = wg % gridDim.x, chunk = wg / gridDim.x;
+    const uint32_t ty0 = band * bg.band_rows, ty1 = min(bg.grid_y, ty0 + bg.band_rows);
+    const uint32_t i = chunk * bg.chunk + threadIdx.x;  // chunk <= GS_FUSED_THREADS (host)
+    const bool own = threadIdx.x < bg.chunk && i < A.n;
+    const bool store = owner && band == 0;
+    ushort4 rc = make_ushort4(0, 0, 0, 0);
+    const uint32_t o = own && A.ids ? A.ids[i] : i;  // the key's index (the caller's)
+    float d = 0.0f;  // view depth (every band's blocks need it for the keys; only band 0 stores it)
+    // (tile-row shard with chunk bounds: a chunk whose bound misses the rows is skipped before its
+    // Gaussians are loaded; it goes through the rest with no pairs)
+    const bool skip = cam.cull && A.cskip[chunk];
+    if (own && !skip) rc = store ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
+    else if (own && store) gs_store_skipped(A, i);
+    if (own && store) {  // for gs_spill_tile: the rect (empty: culled) and depth in walk order
+      rects_out[i] = rc;
+      depths_out[i] = d;
+    }
+#ifdef GS_STAMP
+    if (threadIdx.x == 0) __builtin_amdgcn_s_waitcnt(0);  // (wave 0's preprocess, loads included)
+    STAMP(0, 6);
+#endif
+    uint32_t xw, yh;
+    gs_clip(rc, ty0, ty1, xw, yh);
+    // the chunk's bounding tile rect (within the band): the LDS histogram covers only it, so zeroing
+    // and the reservation scan touch ~100 entries for a spatially coherent chunk instead of the band's
+    uint32_t bx0 = 0xFFFFu, by0 = 0xFFFFu, bx1 = 0u, by1 = 0u;
+    if (yh) {
+      bx0 = xw & 0xFFFFu;
+      bx1 = bx0 + (xw >> 16);
+      by0 = yh & 0xFFFFu;
+      by1 = by0 + (yh >> 16);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      bx0 = min(bx0, (uint32_t)__shfl_xor((int)bx0, off));
+      by0 = min(by0, (uint32_t)__shfl_xor((int)by0, off));
+      bx1 = max(bx1, (uint32_t)__shfl_xor((int)bx1, off));
+      by1 = max(by1, (uint32_t)__shfl_xor((int)by1, off));
+    }
+    // the rects and the inclusive scan of their areas for the workgroup walk: the per-wave partials of
+    // both (rect bounds, area totals) meet behind one barrier
+    const uint32_t area = yh ? (xw >> 16) * (yh >> 16) : 0u;
+    const uint32_t incl = wave_incl_scan(area);
+    if (lane == 0) {
+      s_red[0][wave] = bx0;
+      s_red[1][wave] = by0;
+      s_red[2][wave] = bx1;
+      s_red[3][wave] = by1;
+    }
+    if (lane == 63) s_tot[wave] = incl;
+    if (threadIdx.x < GS_FUSED_THREADS) s_e[threadIdx.x] = make_uint4(xw, yh, o, __float_as_uint(d));
+    __syncthreads();
+    STAMP(0, 7);
+    uint32_t run = incl, P = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) base[j] = c[j] ? atomicAdd(cursor + t[j], c[j]) : 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!c[j]) continue;
-      s_hist[k0 + j * GS_FUSED_WG] = base[j];
-      pairs += c[j];
-      ++res;
-      if (base[j] <= scap && base[j] + c[j] > scap) atomicAdd(fz + 5, 1u);  // (one crossing per spilled tile)
-      if (base[j] + c[j] > 256u) {
-        atomicMax(fz + 1, base[j] + c[j]);
-        if (base[j] <= GS_MID && base[j] + c[j] > GS_MID) atomicAdd(fz + 4, 1u);  // (one crossing per tile)
+    for (uint32_t w = 0; w < GS_FUSED_WG / 64; ++w) {
+      bx0 = min(bx0, s_red[0][w]);
+      by0 = min(by0, s_red[1][w]);
+      bx1 = max(bx1, s_red[2][w]);
+      by1 = max(by1, s_red[3][w]);
+      const uint32_t tw = s_tot[w];
+      run += w < wave ? tw : 0u;
+      P += tw;
+    }
+    if (threadIdx.x < GS_FUSED_THREADS) s_incl[threadIdx.x] = run;
+    // (uniform: in SGPRs, the registers the slice loop keeps)
+    bx0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)bx0);
+    by0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)by0);
+    bx1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)bx1);
+    by1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)by1);
+    P = (uint32_t)__builtin_amdgcn_readfirstlane((int)P);
+    const uint32_t rw = bx1 > bx0 ? bx1 - bx0 : 0u, rh = by1 > by0 ? by1 - by0 : 0u, nt = rw * rh;
+    const uint32_t nsl = (P + GS_FUSED_SLICE - 1u) / GS_FUSED_SLICE;  // slices of this chunk (uniform)
+    if (owner) {
+      if (threadIdx.x == 0) {  // the workgroup's bounding rect (gs_spill_tile; empty: x0 > x1)
+        crect[wg] = nt ? make_ushort4((unsigned short)bx0, (unsigned short)by0, (unsigned short)bx1, (unsigned short)by1)
+                       : make_ushort4(1, 1, 0, 0);
+        // slices 1.. go to the queue (none fit: the owner walks them all itself)
+        uint32_t qb = 0xFFFFFFFFu;
+        if (nsl > 1u) {
+          qb = atomicAdd(fz + GS_FSQ_W + 1, nsl - 1u);
+          if (qb + (nsl - 1u) > fsq_cap) {  // (the part inside the queue is marked taken: helpers skip it)
+            for (uint32_t k = qb; k < fsq_cap && k < qb + (nsl - 1u); ++k)
+              __hip_atomic_store(reinterpret_cast<unsigned long long*>(fsq + k), (unsigned long long)GS_FSQ_TAKEN,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            qb = 0xFFFFFFFFu;
+          } else {
+            for (uint32_t j = 1; j < nsl; ++j)
+              __hip_atomic_store(reinterpret_cast<unsigned long long*>(fsq + qb + j - 1u),
+                                 ((unsigned long long)j << 32) | (wg + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        // published (helpers stop waiting once every owner has; no release fence: an agent-scope one
+        // writes back the XCD's L2. A helper that sees every owner done before it sees its entry keeps
+        // waiting while its index is below the tail; one that leaves early leaves the slice to its owner)
+        atomicAdd(fz + GS_FSQ_W + 2, 1u);
+        s_job[1] = qb;
       }
     }
+    // the slices this pass walks: helpers one; owners slice 0, then each queued slice it can still
+    // claim (or every slice when the queue was full)
+    for (;;) {
+      const uint32_t p0 = slice * GS_FUSED_SLICE, p1 = min(P, p0 + GS_FUSED_SLICE);
+      for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_WG) s_hist[k] = 0;
+      __syncthreads();  // (the scan and the zeroed histogram)
+      STAMP(0, 1);
+      STAMP_SYNC();
+      STAMP(0, 2);
+      uint32_t pk[GS_FUSED_QREG];
+      const uint32_t kept = p1 > p0 ? gs_wg_count_keep(s_incl, s_e, GS_FUSED_THREADS, p0, p1, s_hist, bx0, by0, rw, pk) : 0u;
+      __syncthreads();
+      STAMP(0, 3);
+      // reserve: one returning atomic per touched tile (all of a work-item's issued before any is
+      // used); the LDS entry becomes the run's base
+      const float rcp_rw = 1.0f / (float)max(rw, 1u);
+      for (uint32_t k0 = threadIdx.x; k0 < nt; k0 += 4 * GS_FUSED_WG) {
+        uint32_t c[4], t[4], base[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t k = k0 + j * GS_FUSED_WG;
+          c[j] = k < nt ? s_hist[k] : 0u;
+          uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13 * 2^13: exact after the fix-ups
+          ry = ry * rw > k ? ry - 1 : ry;
+          ry = (ry + 1) * rw <= k ? ry + 1 : ry;
+          t[j] = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) base[j] = c[j] ? atomicAdd(cursor + t[j], c[j]) : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!c[j]) continue;
+          s_hist[k0 + j * GS_FUSED_WG] = base[j];
+          acc_pairs += c[j];
+          ++acc_res;
+          if (base[j] <= scap && base[j] + c[j] > scap) atomicAdd(fz + 5, 1u);  // (one crossing per spilled tile)
+          if (base[j] + c[j] > 256u) {
+            atomicMax(fz + 1, base[j] + c[j]);
+            if (base[j] <= GS_MID && base[j] + c[j] > GS_MID) atomicAdd(fz + 4, 1u);  // (one crossing per tile)
+          }
+        }
+      }
+      __syncthreads();  // every run's base is in s_hist
+      STAMP(0, 4);
+#pragma unroll
+      for (uint32_t c = 0; c < GS_FUSED_QREG; ++c) {
+        if (c < kept) {
+          const uint32_t k = pk[c] & 0x1FFFu, rel = s_hist[k] + ((pk[c] >> 13) & ((1u << GS_KEEP_RB) - 1u));
+          const uint4 e = s_e[pk[c] >> (13u + GS_KEEP_RB)];
+          uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13: exact after the fix-ups
+          ry = ry * rw > k ? ry - 1 : ry;
+          ry = (ry + 1) * rw <= k ? ry + 1 : ry;
+          const uint32_t t = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
+          if (rel < scap) {
+            const unsigned long long key = ((unsigned long long)e.w << 32) | e.z;
+            unsigned long long* dst = tile_slots + (size_t)t * scap + rel;
+            if (GS_NT_SLOTS) __builtin_nontemporal_store(key, dst);
+            else *dst = key;
+          }
+        }
+      }
+      if (!owner) break;
+      // owner: the next of its slices that no helper has taken (uniform through LDS)
+      __syncthreads();  // (every read of s_hist / s_job before they change)
+      if (threadIdx.x == 0) {
+        const uint32_t qb = s_job[1];
+        uint32_t next = 0xFFFFFFFFu;
+        for (uint32_t j = slice + 1; j < nsl; ++j) {
+          if (qb == 0xFFFFFFFFu) {  // queue full: all of them here
+            next = j;
+            break;
+          }
+          if (atomicCAS(&fsq[qb + j - 1u].x, wg + 1u, GS_FSQ_TAKEN) == wg + 1u) {
+            next = j;
+            break;
+          }
+        }
+        s_job[2] = next;
+      }
+      __syncthreads();
+      const uint32_t next = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_job[2]);
+      if (next == 0xFFFFFFFFu) break;
+      slice = next;
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
-    pairs += (uint32_t)__shfl_xor((int)pairs, off);
-    res += (uint32_t)__shfl_xor((int)res, off);
+    acc_pairs += (uint32_t)__shfl_xor((int)acc_pairs, off);
+    acc_res += (uint32_t)__shfl_xor((int)acc_res, off);
   }
+  __syncthreads();
   if (lane == 0) {
-    s_red[0][wave] = pairs;
-    s_red[1][wave] = res;
+    s_red[0][wave] = acc_pairs;
+    s_red[1][wave] = acc_res;
   }
   __syncthreads();
   if (threadIdx.x == 0) {  // per-workgroup partials (the blend's block (0, 0) sums them: no fan-in atomics)
@@ -1045,39 +1234,10 @@ __global__ __launch_bounds__(GS_FUSED_WG) void gs_bin_fused_kernel(SplatCam cam,
       p += s_red[0][w];
       r += s_red[1][w];
     }
-    const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
-    fzp[2 * wg] = p;
-    fzp[2 * wg + 1] = r;
+    const uint32_t fw = blockIdx.y * gridDim.x + blockIdx.x;
+    fzp[2 * fw] = p;
+    fzp[2 * fw + 1] = r;
   }
-  STAMP(0, 4);
-  if (keep) {  // (every run's base is in s_hist: the barrier before the partials' sum)
-#pragma unroll
-    for (uint32_t c = 0; c < GS_FUSED_QREG; ++c) {
-      if (c < kept) {
-        const uint32_t k = pk[c] & 0x1FFFu, rel = s_hist[k] + ((pk[c] >> 13) & ((1u << GS_KEEP_RB) - 1u));
-        const uint4 e = s_e[pk[c] >> (13u + GS_KEEP_RB)];
-        uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13: exact after the fix-ups
-        ry = ry * rw > k ? ry - 1 : ry;
-        ry = (ry + 1) * rw <= k ? ry + 1 : ry;
-        const uint32_t t = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
-        if (rel < scap) {
-          const unsigned long long key = ((unsigned long long)e.w << 32) | e.z;
-          unsigned long long* dst = tile_slots + (size_t)t * scap + rel;
-          if (GS_NT_SLOTS) __builtin_nontemporal_store(key, dst);
-          else *dst = key;
-        }
-      }
-    }
-  } else
-  gs_wg_walk(s_incl, s_e, GS_FUSED_THREADS, P, [&](uint32_t g, uint32_t x, uint32_t y, uint32_t dep) {
-    const uint32_t rel = atomicAdd(s_hist + (y - by0) * rw + (x - bx0), 1u);
-    if (rel < scap) {
-      const unsigned long long key = ((unsigned long long)dep << 32) | g;
-      unsigned long long* dst = tile_slots + (size_t)(y * bg.grid_x + x) * scap + rel;
-      if (GS_NT_SLOTS) __builtin_nontemporal_store(key, dst);
-      else *dst = key;
-    }
-  });
 #ifdef GS_STAMP
   STAMP_SYNC();
   STAMP(0, 5);
@@ -1606,6 +1766,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       fu.fz[5] = 0;
       __threadfence_system();
     }
+    if (blockIdx.x == 0 && blockIdx.y == 0) {  // the slice queue of the front end back to empty
+      const uint32_t used = min(fu.fz[GS_FSQ_W + 1], fu.fsq_cap);
+      for (uint32_t k = tid; k < used; k += GS_BLOCK) fu.fsq[k] = make_uint2(0u, 0u);
+      if (tid == 0) {
+        fu.fz[GS_FSQ_W] = 0;
+        fu.fz[GS_FSQ_W + 1] = 0;
+        fu.fz[GS_FSQ_W + 2] = 0;
+      }
+    }
   }
 #if GS_XCD_REMAP
   // XCD-aware: the workgroups of one XCD blend one horizontal strip of tiles, so the records of the
@@ -2060,6 +2229,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   cam.row_begin = std::min(tile_row_begin, cam.grid_y);
   cam.row_end = std::min(tile_row_end, cam.grid_y);
   if (cam.row_end < cam.row_begin) cam.row_end = cam.row_begin;
+  cam.cull = (g->chunk_bounds && (cam.row_begin > 0 || cam.row_end < cam.grid_y)) ? 1u : 0u;
   const uint32_t tiles = cam.grid_x * cam.grid_y;
 
   if ((e = ensure(w->means2d, (size_t)n * 8))) return e;
@@ -2106,8 +2276,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = hipHostGetDevicePointer((void**)&w->k_dev, w->k_host, 0))) return e;
   }
   if (!w->fz.p) {  // device counters of both front ends, the blend and the spill pool (zero once)
-    if ((e = ensure(w->fz, 64))) return e;
-    if ((e = hipMemsetAsync(w->fz.p, 0, 64, s))) return e;
+    if ((e = ensure(w->fz, 256))) return e;
+    if ((e = hipMemsetAsync(w->fz.p, 0, 256, s))) return e;
   }
   // An earlier frame of this workspace left a spilled tile incomplete (pool exhausted; k_host[9], a
   // device store seen once that frame has run) or met an id >= N (k_host[10]): reported by this call,
@@ -2180,6 +2350,15 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   pa.ids = g->ids;
   pa.dbg_depths = (float*)w->dbg_depths.p;
   pa.bad_ids = w->k_dev + 10;
+  pa.cskip = nullptr;
+  if (cam.cull) {  // chunks whose bound misses the rows: skipped by the front end before their loads
+    const uint32_t nch = (n + 255u) / 256u;
+    if ((e = ensure(w->cskip, nch))) return e;
+    hipLaunchKernelGGL(gs_chunk_cull_kernel, dim3((nch + 255u) / 256u), dim3(256), 0, s, cam,
+                       (const float4*)g->chunk_bounds, nch, (uint8_t*)w->cskip.p);
+    if ((e = hipGetLastError())) return e;
+    pa.cskip = (const uint8_t*)w->cskip.p;
+  }
   if (!publish) {  // the per-Gaussian debug outputs only for a published frame (ptgs_splat_get_buffers)
     pa.radii = nullptr;
     pa.touched = nullptr;
@@ -2200,7 +2379,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
 #define GS_TILE_ORDER 1  // fused frames blend their tiles heaviest first (gs_tile_order)
 #endif
 #ifndef GS_FUSED_RUNS_PER_TILE
-#define GS_FUSED_RUNS_PER_TILE 16u
+#define GS_FUSED_RUNS_PER_TILE 32u  // (C2 Morton order: 6; random order: 51; orbit views up to ~20, where
+                                    // fused measured 0.13 vs 0.24 ms for three launches)
 #endif
   // policy (PTGS_GS_FRONTEND unset): the fused path while frames touch at most
   // GS_FUSED_RUNS_PER_TILE (workgroup, tile) runs per tile (Gaussians in a spatially coherent order:
@@ -2271,7 +2451,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     order = (uint32_t*)w->order.p;
   }
 #endif
-  const GsFused no_fu = {0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order};
+  const GsFused no_fu = {0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order, nullptr, 0u};
 
   auto enqueue_fused = [&]() -> hipError_t {
     hipError_t e2;
@@ -2282,21 +2462,31 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
       if ((e2 = ensure(w->cursor, (size_t)tiles * 4))) return e2;
       if ((e2 = hipMemsetAsync(w->cursor.p, 0, w->cursor.bytes, s))) return e2;
     }
-    const uint32_t nwg = nwg_fused;
+    // owners (bands x chunks) and helpers (bands x GS_FUSED_HELPERS) each publish their partials
+    const uint32_t nwg = nwg_fused + bgrid.bands * GS_FUSED_HELPERS;
     if ((e2 = ensure(w->fzp, (size_t)nwg * 8))) return e2;
+    // slice queue: room for twice the slices of the largest pair count seen (+ one per owner); zero
+    // once here, re-armed by the blend after every frame
+    const uint32_t qcap = std::max<uint32_t>(4096u, 2u * (w->k_host[0] / GS_FUSED_SLICE) + nwg_fused);
+    if (w->fsq.bytes < (size_t)qcap * 8) {
+      if ((e2 = ensure(w->fsq, (size_t)qcap * 8))) return e2;
+      if ((e2 = hipMemsetAsync(w->fsq.p, 0, w->fsq.bytes, s))) return e2;
+    }
+    const uint32_t fsq_cap = (uint32_t)std::min<size_t>(w->fsq.bytes / 8, 0x7FFFFFFFu);
     GsFused fu = {scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
-                  (uint32_t*)w->fzp.p, nwg, order};
+                  (uint32_t*)w->fzp.p, nwg, order, (uint2*)w->fsq.p, fsq_cap};
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers (band 0 stores them for gs_spill_tile)
     fpa.rects = nullptr;
     fpa.depths = nullptr;
     BinGrid fg = bgrid;
     fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
     fg.chunk = GS_FUSED_THREADS;
-    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks + (order ? 1u : 0u)), dim3(GS_FUSED_WG), band_lds, s,
+    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks + GS_FUSED_HELPERS + (order ? 1u : 0u)),
+                       dim3(GS_FUSED_WG), band_lds, s,
                        cam, fpa, fg, scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
                        (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, order,
                        cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x, (ushort4*)w->crect.p, (ushort4*)w->rect.p,
-                       (float*)w->depths.p, w->k_dev);
+                       (float*)w->depths.p, w->k_dev, (uint2*)w->fsq.p, fsq_cap);
     if ((e2 = hipGetLastError())) return e2;
     if ((e2 = mark(1)) || (e2 = mark(2)) || (e2 = mark(3))) return e2;
     unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
@@ -2547,6 +2737,47 @@ hipError_t splat_sort_spatial(const ptgs_gaussians* g, float* means, float* scal
 // pairs: the pair buffer (three launches: a frame of K <= pairs stores every pair) and the spill pool
 // (fused rows: a frame's spilled tiles hold at most K pairs) — a frame of at most `pairs` pairs is always
 // rendered completely, whichever front end runs and whatever its row capacity (hipGraph replays too)
+// ---- chunk bounds (ptgs_gaussians_chunk_bounds) -----------------------------------------------------
+// chunk c = Gaussians [256 c, 256 c + 256): (min x, min y, min z, max |scale|), (max x, max y, max z, 0)
+__global__ __launch_bounds__(256) void gs_chunk_bounds_kernel(const float* __restrict__ means,
+                                                              const float* __restrict__ scales, uint32_t n,
+                                                              float4* __restrict__ out) {
+  __shared__ float s_b[7][4];
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  float b[7] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY, 0.0f};
+  if (i < n) {
+    for (int a = 0; a < 3; ++a) b[a] = b[3 + a] = means[3 * i + a];
+    b[6] = fmaxf(fabsf(scales[3 * i]), fmaxf(fabsf(scales[3 * i + 1]), fabsf(scales[3 * i + 2])));
+  }
+  for (int off = 32; off > 0; off >>= 1)
+    for (int a = 0; a < 3; ++a) {
+      b[a] = fminf(b[a], __shfl_xor(b[a], off));
+      b[3 + a] = fmaxf(b[3 + a], __shfl_xor(b[3 + a], off));
+    }
+  for (int off = 32; off > 0; off >>= 1) b[6] = fmaxf(b[6], __shfl_xor(b[6], off));
+  if ((threadIdx.x & 63u) == 0)
+    for (int a = 0; a < 7; ++a) s_b[a][threadIdx.x >> 6] = b[a];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      for (int a = 0; a < 3; ++a) {
+        b[a] = fminf(b[a], s_b[a][w]);
+        b[3 + a] = fmaxf(b[3 + a], s_b[3 + a][w]);
+      }
+      b[6] = fmaxf(b[6], s_b[6][w]);
+    }
+    out[2 * blockIdx.x] = make_float4(b[0], b[1], b[2], b[6]);
+    out[2 * blockIdx.x + 1] = make_float4(b[3], b[4], b[5], 0.0f);
+  }
+}
+
+hipError_t splat_chunk_bounds(const ptgs_gaussians* g, float* bounds, hipStream_t s) {
+  if (g->count == 0) return hipSuccess;
+  hipLaunchKernelGGL(gs_chunk_bounds_kernel, dim3((g->count + 255u) / 256u), dim3(256), 0, s, g->means, g->scales,
+                     g->count, (float4*)bounds);
+  return hipGetLastError();
+}
+
 hipError_t splat_reserve(SplatWorkspace* w, uint32_t pairs) {
   hipError_t e;
   if ((e = ensure(w->pairs, (size_t)pairs * 8))) return e;

@@ -203,7 +203,7 @@ def render_hybrid_frame(renderer, gaussians: dict, ubo, width: int, height: int,
       1. rank g traces samples g, g + G, ... (spp_total / G of them, SUM) of the whole frame into accum;
       2. reduce-scatter of accum by the ranks' tile rows (reduce_scatter_rows): rank g ends up with the
          full radiance sum of its own rows only;
-      3. their running mean (rgb / count, a = 1) into out's rows, the primary-hit depth;
+      3. their running mean (rgb / count, a = 1) into out's rows, the primary-hit depth of its rows;
       4. the 3DGS splat-over composite of its tile rows (ptgs_splat_gaussians_over, out as "under");
       5. the row gather to rank 0 (gather_rows): out is the composed frame there.
     accum: (H, W, 4) sum buffer; depth: (H, W); out: (H, W, 4). tile_rows: every rank's (begin, end)
@@ -222,8 +222,9 @@ def render_hybrid_frame(renderer, gaussians: dict, ubo, width: int, height: int,
     renderer.trace_camera(ubo, width, height, accum, spp=spp_total // world, frame_stride=stride, mode=ACCUM_SUM,
                           stream=stream)
     reduce_scatter_rows(accum, px, renderer=renderer, stream=stream)
-    renderer.trace_depth(ubo, width, height, depth, stream=stream)
     p0, p1 = px[rank]
+    if p1 > p0:  # the primary-hit depth of this rank's rows only (the composite reads no other)
+        renderer.trace_depth(ubo, width, height, depth, stream=stream, rows=(p0, p1))
     if p1 > p0:
         with _on_stream(out, stream):
             out[p0:p1] = resolve_mean(accum[p0:p1])

@@ -40,6 +40,7 @@ def _gaussians(g: dict) -> Gaussians:
     gs.opacities, gs.colors = _ptr(g["opacities"]), _ptr(g["colors"])
     gs.count = int(g["means"].shape[0])
     gs.ids = _ptr(g.get("ids"))
+    gs.chunk_bounds = _ptr(g.get("chunk_bounds"))
     return gs
 
 
@@ -117,8 +118,14 @@ class Renderer:
                                        _stream(stream))
         self._chk(rc, "ptgs_trace_torus")
 
-    def trace_depth(self, ubo: Ubo, width: int, height: int, depth, stream=None):
-        """Primary-hit view depth per pixel (+inf on a miss) into a device float[H, W] tensor."""
+    def trace_depth(self, ubo: Ubo, width: int, height: int, depth, stream=None, rows=None):
+        """Primary-hit view depth per pixel (+inf on a miss) into a device float[H, W] tensor; rows =
+        (begin, end) pixel rows traces only those (ptgs_trace_depth_rows)."""
+        if rows is not None:
+            rc = self.lib.ptgs_trace_depth_rows(self._h, C.byref(ubo), width, height, int(rows[0]), int(rows[1]),
+                                                _ptr(depth), _stream(stream))
+            self._chk(rc, "ptgs_trace_depth_rows")
+            return
         rc = self.lib.ptgs_trace_depth(self._h, C.byref(ubo), width, height, _ptr(depth), _stream(stream))
         self._chk(rc, "ptgs_trace_depth")
 
@@ -265,6 +272,17 @@ class Renderer:
                                                   _ptr(out["rotations"]), _ptr(out["opacities"]), _ptr(out["colors"]),
                                                   _ptr(out["ids"]), _stream(stream))
         self._chk(rc, "ptgs_gaussians_sort_spatial")
+        return out
+
+    def gaussians_chunk_bounds(self, g: dict, stream=None):
+        """ptgs_gaussians_chunk_bounds: per chunk of 256 Gaussians the box of the means and the largest
+        scale (float32 tensor [chunks, 8]); put it in g["chunk_bounds"] so that tile-row-restricted
+        frames skip the chunks that cannot reach their rows."""
+        import torch
+        n = int(g["means"].shape[0])
+        out = torch.empty((max(1, (n + 255) // 256), 8), dtype=torch.float32, device=g["means"].device)
+        self._chk(self.lib.ptgs_gaussians_chunk_bounds(self._h, C.byref(_gaussians(g)), _ptr(out), _stream(stream)),
+                  "ptgs_gaussians_chunk_bounds")
         return out
 
     def splat_status(self, stream=None) -> SplatStatus:

@@ -114,8 +114,10 @@ class _OracleRenderer:
         self.oracle.trace_camera(self.scene.desc(), ubo, width, height, acc, spp=spp, frame_stride=frame_stride,
                                  mode=mode, rows=rows)
 
-    def trace_depth(self, ubo, width, height, depth, stream=None):
-        depth[...] = torch.from_numpy(self.oracle.trace_depth(self.scene.desc(), ubo, width, height))
+    def trace_depth(self, ubo, width, height, depth, stream=None, rows=None):
+        d = torch.from_numpy(self.oracle.trace_depth(self.scene.desc(), ubo, width, height))
+        r0, r1 = (0, height) if rows is None else rows
+        depth[r0:r1] = d[r0:r1]  # (rows outside are left untouched, as ptgs_trace_depth_rows)
 
     def splat_gaussians(self, g, ubo, width, height, out, bg=(0.0, 0.0, 0.0), tile_rows=None, stream=None,
                         want_stats=False, over=None):

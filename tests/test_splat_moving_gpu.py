@@ -275,3 +275,40 @@ def test_gaussians_out_of_range_ids_are_reported(native_lib, oracle_lib):
         assert U.rel_l2(out.cpu().numpy(), ref["image"]) < 1e-4
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("radius", [8.0, 5.0, 2.5, 20.0])
+def test_gaussians_tile_row_bands_with_chunk_bounds(native_lib, oracle_lib, radius):
+    """a tile-row-restricted frame with ptgs_gaussians.chunk_bounds skips the
+    256-Gaussian chunks whose conservative screen bound misses its rows before loading them. Over
+    camera distances from outside the cloud to inside it (chunks straddling the near plane), every band
+    of 4 keeps the oracle's keys / values / ranges / radii / tiles touched of those rows bit for bit,
+    and the bands compose the full frame exactly (both front ends: frame 0 three launches, then fused)."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H, n = 480, 270, 20_000
+    g = Y.gaussians_c2(n, seed=51)
+    ubo = orbit_ubo(5, W, H, radius=radius)
+    gy = (H + 15) // 16
+    bands = [(0, 4), (4, 9), (9, 13), (13, gy)]
+    r = Renderer(0, publish_splat_buffers=True)
+    try:
+        dg = r.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        dgb = dict(dg, chunk_bounds=r.gaussians_chunk_bounds(dg))
+        full = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        r.splat_gaussians(dg, ubo, W, H, full, bg=(0.1, 0.2, 0.3), want_stats=True)
+        for frame in range(2):
+            comp = torch.full_like(full, -7.0)
+            for rows in bands:
+                st = r.splat_gaussians(dgb, ubo, W, H, comp, bg=(0.1, 0.2, 0.3), tile_rows=rows, want_stats=True)
+                torch.cuda.synchronize()
+                ref = oracle_lib.splat_gaussians(g, ubo, W, H, bg=(0.1, 0.2, 0.3), tile_rows=rows)
+                b = r.splat_buffers()
+                assert st.num_rendered == ref["K"], (rows, st.num_rendered, ref["K"])
+                np.testing.assert_array_equal(_read(r, b.sorted_keys, ref["K"], np.uint64), ref["keys"])
+                np.testing.assert_array_equal(_read(r, b.sorted_values, ref["K"], np.uint32), ref["vals"])
+                np.testing.assert_array_equal(_read(r, b.tile_ranges, 2 * b.num_tiles, np.uint32), ref["ranges"])
+                np.testing.assert_array_equal(_read(r, b.radii, n, np.int32), ref["radii"])
+                np.testing.assert_array_equal(_read(r, b.tiles_touched, n, np.uint32), ref["touched"])
+            assert torch.equal(comp, full), f"bands != full frame (frame {frame})"
+    finally:
+        r.close()
