@@ -59,18 +59,19 @@ struct ptgs_ctx {
 
 namespace {
 
-// 4-wide collapse whose worst-case traversal stack fits PTGS_STACK with fan-out `fan` (a 2-wide
-// "collapse" needs the BVH2 depth, which the builders keep below PTGS_STACK)
-static bool collapse_fit(const std::vector<float>& n2, std::vector<float>& n4, uint32_t& num4, uint32_t& dep4, int fan) {
-  uint32_t need = 0;
+// 4-wide collapse whose worst-case traversal stack fits PTGS_STACK_TOTAL (LDS + overflow) with fan-out
+// `fan` (a 2-wide "collapse" needs the BVH2 depth, which the builders keep below PTGS_STACK)
+static bool collapse_fit(const std::vector<float>& n2, std::vector<float>& n4, uint32_t& num4, uint32_t& dep4, int fan,
+                         uint32_t& need) {
+  need = 0;
   ptgs::collapse_bvh4(n2, n4, num4, need, dep4, fan);
-  return need < PTGS_STACK;
+  return need < PTGS_STACK_TOTAL;
 }
 
-// (leaf size, fan-out) tried in this order until the tree's worst-case stack need fits PTGS_STACK:
-// a large scene whose 3-triangle-leaf tree is too deep for a 4-wide collapse is rebuilt with 4-triangle
-// leaves before the fan-out is narrowed (C5's 1M-triangle atrium: a 2-wide fallback traced at 1.38
-// Grays/s, the 4-triangle-leaf 4-wide tree at ~2.1)
+// (leaf size, fan-out) tried in this order until the tree's worst-case stack need fits PTGS_STACK_TOTAL:
+// a scene whose 3-triangle-leaf tree is too deep for a 4-wide collapse is rebuilt with 4-triangle
+// leaves before the fan-out is narrowed (a 2-wide fallback traced C5 at 1.38 Grays/s, the
+// 4-triangle-leaf 4-wide tree at ~2.1; with the stack overflow C5 keeps 3-triangle leaves: need 40)
 static const int kBvhTries[][2] = {{PTGS_BVH_LEAF, 4}, {PTGS_BVH_LEAF + 1, 4}, {PTGS_BVH_LEAF, 3}, {PTGS_BVH_LEAF, 2}};
 
 int fail(ptgs_ctx* c, int code, const char* fmt, ...) {
@@ -333,7 +334,7 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     const int tries = lbvh ? 3 : (int)(sizeof(kBvhTries) / sizeof(kBvhTries[0]));
     int built_leaf = -1;
     float4* n4 = nullptr;
-    uint32_t num4 = 0, need = PTGS_STACK, dep4 = 0;
+    uint32_t num4 = 0, need = PTGS_STACK_TOTAL, dep4 = 0;
     for (int k = 0; k < tries; ++k) {
       const int leaf = lbvh ? 0 : kBvhTries[k][0], fan = lbvh ? 4 - k : kBvhTries[k][1];
       if (leaf != built_leaf) {  // (re)build the BVH2
@@ -356,9 +357,9 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
       e = collapse_bvh4_gpu(g.nodes, g.num_nodes, fan, &n4, &num4, &need, &dep4);
       auto t1 = std::chrono::steady_clock::now();
       ms += (float)std::chrono::duration<double, std::milli>(t1 - t0).count();  // build_ms includes it
-      if (e != hipSuccess || need < PTGS_STACK) break;
+      if (e != hipSuccess || need < PTGS_STACK_TOTAL) break;
     }
-    if (e == hipSuccess && need >= PTGS_STACK) e = hipErrorNotSupported;
+    if (e == hipSuccess && need >= PTGS_STACK_TOTAL) e = hipErrorNotSupported;
     if (e == hipSuccess || e == hipErrorNotSupported) {
       (void)hipFree(g.nodes);
       g.nodes = n4;
@@ -372,6 +373,7 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
       s.nodes = g.nodes;
       s.tris = g.tris;
       s.tri_flags = g.tri_flags;
+      s.deep_stack = need >= PTGS_STACK ? 1 : 0;
       c->info.num_bvh_nodes = g.num_nodes;
       c->info.bvh_depth = g.depth;
       c->info.max_leaf_size = (c->flags & PTGS_FLAG_GPU_LBVH) ? 4u : g.max_leaf;
@@ -393,7 +395,7 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     auto t0 = std::chrono::steady_clock::now();
     BvhOut bvh;
     std::vector<float> n4;
-    uint32_t num4 = 0, dep4 = 0;
+    uint32_t num4 = 0, dep4 = 0, need = PTGS_STACK_TOTAL;
     int built_leaf = -1;
     bool fits = false;
     for (const auto& tr : kBvhTries) {
@@ -402,10 +404,11 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
         built_leaf = tr[0];
         if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
       }
-      if ((fits = collapse_fit(bvh.nodes, n4, num4, dep4, tr[1]))) break;
+      if ((fits = collapse_fit(bvh.nodes, n4, num4, dep4, tr[1], need))) break;
     }
     auto t1 = std::chrono::steady_clock::now();
     if (!fits) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
+    s.deep_stack = need >= PTGS_STACK ? 1 : 0;
     if ((rc = upload(c, (const float4*)n4.data(), n4.size() / 4, &s.nodes))) return rc;
     bvh.num_nodes = num4;
     bvh.depth = dep4;

@@ -41,6 +41,8 @@ struct DevScene {
   const float4* blue_noise;
   DevTextures tex;                // global_textures[] (texture.h)
   int32_t uses_textures;          // some material has a texture index > 0: launch the TEX kernels
+  int32_t deep_stack;             // the tree's worst-case stack need exceeds PTGS_STACK: launch the
+                                  // kernels with the stack overflow (OVF = PTGS_STACK_OVF)
   uint32_t num_light_cdf;
   uint32_t num_plights;
   int32_t bn_size;
@@ -72,14 +74,22 @@ struct TraversalCounters {
 // Traversal stack: PTGS_STACK entries per work-item in LDS, interleaved across the 256 work-items
 // of a workgroup (entry k of lane t at [k * 256 + t]: conflict-free ds_read/ds_write_b32).
 // 39 x 256 x 4 B = 39 KiB per workgroup (+ 1 KiB of slot rings in the wavefront kernels: 4
-// workgroups = 16 waves per CU fill the 160 KiB LDS). A 4-wide node pushes up to 3 entries: the
-// scene upload (api.cpp kBvhTries) rebuilds with 4-triangle leaves, then caps the fan-out, until the
-// tree's worst-case stack need fits (4-wide, else 3-, else 2-wide, which the builder's depth bound
-// fits). C3's 250k-triangle atrium fits with 3-triangle leaves; C5's 1M-triangle atrium takes the
-// 4-triangle-leaf 4-wide tree.
+// workgroups = 16 waves per CU fill the 160 KiB LDS). Deeper entries, up to PTGS_STACK_TOTAL, go
+// to a per-work-item overflow: private (scratch) memory in the megakernel, a global column in the
+// wavefront kernels. A 4-wide node pushes up to 3 entries: the scene upload (api.cpp kBvhTries)
+// rebuilds with 4-triangle leaves, then caps the fan-out, only if the tree's worst-case stack need
+// exceeds PTGS_STACK_TOTAL. C3's 250k-triangle atrium needs 38 with 3-triangle leaves, C5's
+// 1M-triangle atrium 40 (tools/native/bvh_need.cpp): both keep 3-triangle leaves and 4-wide nodes.
+// The overflow is compiled only into the DEEP kernel instantiations (DevScene::deep_stack: need >=
+// PTGS_STACK), launched for C5's tree; C3's runs the LDS-only traversal (the overflow's test per push /
+// pop cost 3.4% on C3 even unused, tools/ab_pt.py).
 #ifndef PTGS_STACK
 #define PTGS_STACK 39
 #endif
+#ifndef PTGS_STACK_OVF
+#define PTGS_STACK_OVF 9  // overflow entries beyond the LDS part
+#endif
+#define PTGS_STACK_TOTAL (PTGS_STACK + PTGS_STACK_OVF)
 #define PTGS_BLOCK 256
 
 PTGS_HD float i2f(int x) { union { int i; float f; } c; c.i = x; return c.f; }
@@ -259,7 +269,9 @@ __device__ __forceinline__ void cswap4(Box4& b, int i, int j) {
   b.c[i] = sw ? cj : ci; b.c[j] = sw ? ci : cj;
 }
 
-template <bool STATS, bool TEX, int SS = PTGS_BLOCK>  // SS: the LDS stack's stride (work-items sharing it)
+// SS: the LDS stack's stride (work-items sharing it); OVF: overflow entries beyond the LDS part (0 for
+// a tree whose stack need fits PTGS_STACK: the overflow's branches and scratch cost 3.4% on C3)
+template <bool STATS, bool TEX, int SS = PTGS_BLOCK, int OVF = PTGS_STACK_OVF>
 __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
                                              TraversalCounters& cnt) {
   Hit h; h.t = r.tmax; h.u = 0.f; h.v = 0.f; h.gid = 0xffffffffu; h.slot = 0;
@@ -272,8 +284,17 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   // candidate, so visiting order changes neither the hit nor the image.
   const int DONE = 0x7fffffff;
   int leaf = DONE;
-  auto push = [&](int x) { stack[(sp++) * SS] = x; };
-  auto pop = [&]() -> int { return sp ? stack[(--sp) * SS] : DONE; };
+  int ovf[OVF > 0 ? OVF : 1];  // entries beyond the LDS part (private: scratch)
+  auto push = [&](int x) {
+    if (OVF == 0 || sp < PTGS_STACK) stack[sp * SS] = x;
+    else ovf[sp - PTGS_STACK] = x;
+    ++sp;
+  };
+  auto pop = [&]() -> int {
+    if (!sp) return DONE;
+    --sp;
+    return (OVF == 0 || sp < PTGS_STACK) ? stack[sp * SS] : ovf[sp - PTGS_STACK];
+  };
   // (a register-cached stack top that hides the LDS read behind the node fetch measured -0.8%)
   for (;;) {
     while (node >= 0 && node != DONE) {
@@ -307,11 +328,16 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   }
 }
 
-template <bool STATS, bool TEX, int SS = PTGS_BLOCK>  // SS: the LDS stack's stride (work-items sharing it)
+template <bool STATS, bool TEX, int SS = PTGS_BLOCK, int OVF = PTGS_STACK_OVF>  // (as trace_closest)
 __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint32_t seed, int* stack,
                                           TraversalCounters& cnt) {
   int sp = 0;
   int node = 0;
+  int ovf[OVF > 0 ? OVF : 1];  // entries beyond the LDS part (private: scratch)
+  auto pop_nz = [&]() -> int {  // sp > 0
+    --sp;
+    return (OVF == 0 || sp < PTGS_STACK) ? stack[sp * SS] : ovf[sp - PTGS_STACK];
+  };
   while (true) {
     while (node >= 0) {
       Box4 b;
@@ -324,12 +350,18 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (b.tn[j] != __builtin_huge_valf()) {
-          if (!have) { next = b.c[j]; have = true; }
-          else stack[(sp++) * SS] = b.c[j];
+          if (!have) {
+            next = b.c[j];
+            have = true;
+          } else {
+            if (OVF == 0 || sp < PTGS_STACK) stack[sp * SS] = b.c[j];
+            else ovf[sp - PTGS_STACK] = b.c[j];
+            ++sp;
+          }
         }
       if (!have) {
         if (sp == 0) return false;
-        node = stack[(--sp) * SS];
+        node = pop_nz();
         continue;
       }
       node = next;
@@ -350,7 +382,7 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
       return true;
     }
     if (sp == 0) return false;
-    node = stack[(--sp) * SS];
+    node = pop_nz();
   }
 }
 
@@ -533,13 +565,13 @@ __device__ __forceinline__ void shadow_towards(ShadowQuery& q, v3 o, v3 light_po
   q.tmax = dist - 0.005f;
 }
 
-template <bool STATS, bool TEX, int SS = PTGS_BLOCK>  // SS: the LDS stack's stride (work-items sharing it)
+template <bool STATS, bool TEX, int SS = PTGS_BLOCK, int OVF = PTGS_STACK_OVF>  // (as trace_closest)
 __device__ __forceinline__ void resolve_shadow(ShadeCtx& c, v3& color, uint32_t seed, const ShadowQuery& q,
                                                TraversalCounters& cnt) {
   if (!(q.flags & SQ_TRACE)) return;
   c.shadow_rays++;
   const Ray r = make_ray(q.o, q.d, 0.001f, q.tmax);
-  float vis = trace_any<STATS, TEX, SS>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
+  float vis = trace_any<STATS, TEX, SS, OVF>(*c.sc, r, seed, c.stack, cnt) ? 0.0f : 1.0f;
   vis = fmaxx(vis, q.trans);
   if (vis > 0.0f && (q.flags & SQ_VALID)) {
     v3 contrib = (q.pre * vis) * q.post;

@@ -79,7 +79,8 @@ __host__ __device__ __forceinline__ uint32_t pt_lanes_log2(uint32_t spp) {
   return (PTGS_PT_LPP >= 4 && spp >= 4u) ? 2u : (PTGS_PT_LPP >= 2 && spp >= 2u) ? 1u : 0u;
 }
 
-template <bool STATS, bool TEX>
+// DEEP: the traversal with the stack overflow (DevScene::deep_stack)
+template <bool STATS, bool TEX, bool DEEP>
 __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kernel(DevScene sc, CamParams cp, float4* __restrict__ accum,
                                                         uint32_t W, uint32_t H, uint32_t row0, uint32_t row1,
                                                         uint32_t spp, uint32_t frame0, uint32_t stride,
@@ -178,13 +179,13 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
         p.depth = depth;
         Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
         ext_rays++;
-        Hit h = trace_closest<STATS, TEX, PTGS_PT_WG>(sc, ray, p.seed, c.stack, tc);
+        Hit h = trace_closest<STATS, TEX, PTGS_PT_WG, DEEP ? PTGS_STACK_OVF : 0>(sc, ray, p.seed, c.stack, tc);
         if (STATS && h.gid != 0xffffffffu) tc.hits++;
         ShadowQuery q;
         q.flags = 0;
         if (h.gid == 0xffffffffu) miss<false>(cp, p);
         else closest_hit<false, TEX>(c, p, ray, h, q);
-        resolve_shadow<STATS, TEX, PTGS_PT_WG>(c, p.color, p.seed, q, tc);  // NEE visibility after shading
+        resolve_shadow<STATS, TEX, PTGS_PT_WG, DEEP ? PTGS_STACK_OVF : 0>(c, p.color, p.seed, q, tc);  // NEE visibility after shading
         acc = acc + p.color * thr;
         acc = vmin(acc, 5.0f);
         if (p.hit_flag < 0.0f) break;
@@ -244,7 +245,7 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
 #ifndef PTGS_TORUS_MIN_WAVES
 #define PTGS_TORUS_MIN_WAVES 4
 #endif
-template <bool STATS, bool TEX>
+template <bool STATS, bool TEX, bool DEEP>
 __global__ __launch_bounds__(256, TEX ? 1 : PTGS_TORUS_MIN_WAVES) void pt_torus_kernel(DevScene sc, CamParams cp, TorusParams tp,
                                                        const ptgs_ray_sample* __restrict__ samples,
                                                        uint32_t n, uint32_t side, uint32_t frame,
@@ -303,13 +304,13 @@ __global__ __launch_bounds__(256, TEX ? 1 : PTGS_TORUS_MIN_WAVES) void pt_torus_
       }
       Ray ray = make_ray(p.next_o, p.next_d, depth == 0 ? 0.0f : 0.001f, 10000.0f);
       ext_rays++;
-      Hit h = trace_closest<STATS, TEX>(sc, ray, p.seed, c.stack, tc);
+      Hit h = trace_closest<STATS, TEX, PTGS_BLOCK, DEEP ? PTGS_STACK_OVF : 0>(sc, ray, p.seed, c.stack, tc);
       if (STATS && h.gid != 0xffffffffu) tc.hits++;
       ShadowQuery q;
       q.flags = 0;
       if (h.gid == 0xffffffffu) miss<true>(cp, p);
       else closest_hit<true, TEX>(c, p, ray, h, q);
-      resolve_shadow<STATS, TEX>(c, p.color, p.seed, q, tc);
+      resolve_shadow<STATS, TEX, PTGS_BLOCK, DEEP ? PTGS_STACK_OVF : 0>(c, p.color, p.seed, q, tc);
       if (depth == 0) {
         fpos = p.hit_pos;
         fflag = p.hit_flag;
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(256, TEX ? 1 : PTGS_TORUS_MIN_WAVES) void pt_torus_
 // Primary-hit depth: the camera ray of raygen_camera.rgen:25-41 through the pixel centre (no
 // jitter), closest hit with the frame's any-hit seed (index + frame_count * 719393, :21); depth =
 // view-space distance -(view * hit).z of the hit point, +inf on a miss. One work-item per pixel.
-template <bool TEX>
+template <bool TEX, bool DEEP>
 __global__ __launch_bounds__(256) void pt_depth_kernel(DevScene sc, CamParams cp, ViewMat vm, float* __restrict__ depth,
                                                        uint32_t W, uint32_t H, uint32_t row0, uint32_t row1,
                                                        uint32_t frame) {
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(256) void pt_depth_kernel(DevScene sc, CamParams cp
   const v3 ro = mk3(origin.x, origin.y, origin.z);
   const v3 rd = normalize3(mk3(direction.x, direction.y, direction.z));
   const Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
-  const Hit h = trace_closest<false, TEX>(sc, ray, seed, s_stack + threadIdx.x, tc);
+  const Hit h = trace_closest<false, TEX, PTGS_BLOCK, DEEP ? PTGS_STACK_OVF : 0>(sc, ray, seed, s_stack + threadIdx.x, tc);
   float d = __builtin_huge_valf();
   if (h.gid != 0xffffffffu) {
     const v3 hp = ro + rd * h.t;
@@ -467,9 +468,14 @@ hipError_t launch_pt_camera(const DevScene& sc, const CamParams& cp, float* accu
     cost = ps->cost;
   }
 #endif
-  // (STATS, TEX) instantiations: TEX only for scenes whose materials reference textures
-  auto k = stats ? (sc.uses_textures ? pt_camera_kernel<true, true> : pt_camera_kernel<true, false>)
-                 : (sc.uses_textures ? pt_camera_kernel<false, true> : pt_camera_kernel<false, false>);
+  // (STATS, TEX, DEEP) instantiations: TEX only for scenes whose materials reference textures, DEEP only
+  // for trees deeper than the LDS stack
+  static void (*const ks[8])(DevScene, CamParams, float4*, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
+                             uint32_t, uint32_t, unsigned long long*, const uint32_t*, uint32_t*) = {
+      pt_camera_kernel<false, false, false>, pt_camera_kernel<false, false, true>, pt_camera_kernel<false, true, false>,
+      pt_camera_kernel<false, true, true>,   pt_camera_kernel<true, false, false>, pt_camera_kernel<true, false, true>,
+      pt_camera_kernel<true, true, false>,   pt_camera_kernel<true, true, true>};
+  auto k = ks[(stats ? 4 : 0) + (sc.uses_textures ? 2 : 0) + (sc.deep_stack ? 1 : 0)];
   hipLaunchKernelGGL(k, grid, block, 0, stream, sc, cp, (float4*)accum, W, H, row0, row1, spp, frame0, stride, mode,
                      counters, order, cost);
   return hipGetLastError();
@@ -480,7 +486,8 @@ hipError_t launch_pt_depth(const DevScene& sc, const CamParams& cp, const ViewMa
   row1 = row1 < H ? row1 : H;
   if (row1 <= row0) return hipSuccess;
   dim3 grid((W + 15u) / 16u, (row1 - row0 + 15u) / 16u);
-  auto k = sc.uses_textures ? pt_depth_kernel<true> : pt_depth_kernel<false>;
+  auto k = sc.uses_textures ? (sc.deep_stack ? pt_depth_kernel<true, true> : pt_depth_kernel<true, false>)
+                           : (sc.deep_stack ? pt_depth_kernel<false, true> : pt_depth_kernel<false, false>);
   hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, sc, cp, vm, depth, W, H, row0, row1, frame);
   return hipGetLastError();
 }
@@ -491,8 +498,12 @@ hipError_t launch_pt_torus(const DevScene& sc, const CamParams& cp, const TorusP
   if (n == 0) return hipSuccess;
   dim3 grid((n + 255u) / 256u);
   dim3 block(256);
-  auto k = stats ? (sc.uses_textures ? pt_torus_kernel<true, true> : pt_torus_kernel<true, false>)
-                 : (sc.uses_textures ? pt_torus_kernel<false, true> : pt_torus_kernel<false, false>);
+  static void (*const ks[8])(DevScene, CamParams, TorusParams, const ptgs_ray_sample*, uint32_t, uint32_t, uint32_t,
+                             ptgs_hitdata*, unsigned long long*) = {
+      pt_torus_kernel<false, false, false>, pt_torus_kernel<false, false, true>, pt_torus_kernel<false, true, false>,
+      pt_torus_kernel<false, true, true>,   pt_torus_kernel<true, false, false>, pt_torus_kernel<true, false, true>,
+      pt_torus_kernel<true, true, false>,   pt_torus_kernel<true, true, true>};
+  auto k = ks[(stats ? 4 : 0) + (sc.uses_textures ? 2 : 0) + (sc.deep_stack ? 1 : 0)];
   hipLaunchKernelGGL(k, grid, block, 0, stream, sc, cp, tp, samples, n, side, frame, hits, counters);
   return hipGetLastError();
 }

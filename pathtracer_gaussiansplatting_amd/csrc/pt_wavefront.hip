@@ -117,8 +117,8 @@ __device__ __forceinline__ void ss_fill(SlotStream& s, const uint8_t* __restrict
 }
 
 // Traversal stack of the extend / shadow kernels: the first WF_LDS_STACK entries in LDS (interleaved
-// by work-item, as pt_device.h), deeper entries (rare: C3's tree needs up to 34, C5's 38) in a
-// per-work-item global overflow area. A shorter LDS stack buys occupancy (LDS-bound otherwise).
+// by work-item, as pt_device.h), deeper entries up to PTGS_STACK_TOTAL (rare: C3's tree needs up to
+// 38, C5's 40) in a per-work-item global overflow area. A shorter LDS stack buys occupancy.
 #ifndef PTGS_WF_AH_CALL
 // textured any-hit inlined (true: out of line, pt_device.h anyhit_accept_call — round 2's workaround for
 // the SLP miscompile that build.py now avoids with -slp-vectorize-hor=false)
@@ -144,13 +144,13 @@ struct TravStack {
   uint32_t ostride;
   int sp;
   __device__ __forceinline__ void push(int v) {
-    if (N >= PTGS_STACK || sp < N) lds[sp * PTGS_BLOCK] = v;
+    if (N >= PTGS_STACK_TOTAL || sp < N) lds[sp * PTGS_BLOCK] = v;
     else ovf[(size_t)(sp - N) * ostride] = v;
     ++sp;
   }
   __device__ __forceinline__ int pop_nz() {  // sp > 0
     --sp;
-    if (N >= PTGS_STACK || sp < N) return lds[sp * PTGS_BLOCK];
+    if (N >= PTGS_STACK_TOTAL || sp < N) return lds[sp * PTGS_BLOCK];
     return ovf[(size_t)(sp - N) * ostride];
   }
 };
@@ -621,7 +621,7 @@ hipError_t launch_pt_wavefront(WfWorkspace& w, const DevScene& sc, const CamPara
   // the per-depth "work pending" words (2 per depth), then the partial counts [WF_NCNT][part_stride]
   if ((e = wf_ensure(w.part, w.part_bytes, ((size_t)WF_NCNT * a.part_stride + 64) * 4, true, s))) return e;
   {  // traversal-stack overflow: the entries beyond the LDS part, per work-item of the largest grid
-    const int deep = PTGS_STACK - std::min(PTGS_WF_LDS_EXT, PTGS_WF_LDS_SHADOW);
+    const int deep = PTGS_STACK_TOTAL - std::min(PTGS_WF_LDS_EXT, PTGS_WF_LDS_SHADOW);
     const size_t grid_tmax = (Pmax + 4u * trace_run - 1u) / (4u * trace_run);
     if (deep > 0 && (e = wf_ensure(w.ovf, w.ovf_bytes, grid_tmax * 256u * (size_t)deep * 4u, false, s))) return e;
     a.ovf = deep > 0 ? (int*)w.ovf : nullptr;

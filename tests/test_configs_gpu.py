@@ -178,9 +178,10 @@ def test_c5_mesh_gpu_sah_build(renderer):
     assert info_g.num_triangles == info_h.num_triangles >= 1_000_000
     assert np.array_equal(nodes_g, nodes_h), f"{int(np.count_nonzero(np.any(nodes_g != nodes_h, 1)))} nodes differ"
     assert _leaf_sets_equal(nodes_h, tris_h, tris_g)
-    # the tree stays 4-wide (api.cpp kBvhTries: 4-triangle leaves before a narrower fan-out; a 2-wide
-    # fallback, ~500k nodes, traced C5 at 0.57x): fewer nodes than a third of the leaves' triangles
-    assert info_h.max_leaf_size == info_g.max_leaf_size <= 4
+    # the tree keeps 3-triangle leaves and 4-wide nodes (worst-case stack need 40:
+    # the 39 LDS entries + the traversal stack's overflow, PTGS_STACK_TOTAL; a 2-wide fallback, ~500k
+    # nodes, traced C5 at 0.57x): fewer nodes than a third of the leaves' triangles
+    assert info_h.max_leaf_size == info_g.max_leaf_size <= 3
     assert info_g.num_bvh_nodes < info_g.num_triangles // 3, info_g.num_bvh_nodes
     print(f"1M tris: host SAH {info_h.build_ms:.1f} ms, GPU SAH {info_g.build_ms:.2f} ms, "
           f"{info_g.num_bvh_nodes} 4-wide nodes, depth {info_g.bvh_depth}")
