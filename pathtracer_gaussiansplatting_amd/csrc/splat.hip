@@ -39,6 +39,10 @@ namespace ptgs {
 #define GS_BLOCK_Y 16
 #define GS_BLOCK (GS_BLOCK_X * GS_BLOCK_Y)
 
+#ifndef GS_TIGHT_BIN
+#define GS_TIGHT_BIN 1  // timed frames bin by the alpha box (SplatCam::tight)
+#endif
+
 struct SplatCam {
   float view[16];
   float mvp[16];  // proj * view
@@ -48,6 +52,7 @@ struct SplatCam {
   uint32_t grid_x, grid_y;
   uint32_t row_begin, row_end;  // tile rows
   uint32_t cull;                // tile rows restricted and chunk bounds given: PreArgs.cskip is valid
+  uint32_t tight;               // bin by the alpha box (frames without stats / published buffers)
 };
 
 struct DevBuf {
@@ -265,6 +270,23 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   int rmax_y = min((int)cam.grid_y, max(0, (int)((pimg.y + (float)r + (float)(GS_BLOCK_Y - 1)) / (float)GS_BLOCK_Y)));
   rmin_y = max(rmin_y, (int)cam.row_begin);
   rmax_y = min(rmax_y, (int)cam.row_end);
+  // (ex, ey): half-extents of the ellipse where alpha >= 1/255 can hold (power >= -ln(255 o), minus a
+  // 1e-3 margin, +1% and +0.01 px): the blend skips whole 8x8 pixel blocks outside that box
+  const float skip = -(log2x(255.0f * con.w) * 0.69314718055994531f) - 0.001f;
+  const float sq = -2.0f * skip;
+  const float ex = sq > 0.0f ? sqrtx(sq * ca) * 1.01f + 0.01f : -1.0f;
+  const float ey = sq > 0.0f ? sqrtx(sq * cc) * 1.01f + 0.01f : -1.0f;
+  if (cam.tight) {
+    // Timed frames bin each Gaussian only to the tiles its alpha box overlaps (pixel x in [16 t, 16 t +
+    // 15]); the reference's 3-sigma rectangle (kept for stats and published buffers) also holds tiles
+    // where no pixel reaches alpha 1/255: 29% of C2's pairs. The blend skips such a pair (alpha 0:
+    // T and colour unchanged, exactly), so the image is the same, bit for bit.
+    if (!(sq > 0.0f)) return none;
+    rmin_x = max(rmin_x, (int)__builtin_ceilf((pimg.x - ex - (float)(GS_BLOCK_X - 1)) * (1.0f / GS_BLOCK_X)));
+    rmax_x = min(rmax_x, (int)__builtin_floorf((pimg.x + ex) * (1.0f / GS_BLOCK_X)) + 1);
+    rmin_y = max(rmin_y, (int)__builtin_ceilf((pimg.y - ey - (float)(GS_BLOCK_Y - 1)) * (1.0f / GS_BLOCK_Y)));
+    rmax_y = min(rmax_y, (int)__builtin_floorf((pimg.y + ey) * (1.0f / GS_BLOCK_Y)) + 1);
+  }
   int area = (rmax_x - rmin_x) * (rmax_y - rmin_y);
   if (rmax_x <= rmin_x || rmax_y <= rmin_y || area == 0) return none;
   const ushort4 rect = make_ushort4((unsigned short)rmin_x, (unsigned short)rmin_y, (unsigned short)rmax_x,
@@ -284,13 +306,8 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   // Blend record (3 x float4), the form the blend loop consumes:
   //   (x, y, A, B), (C, log2 o, r, g), (b, ex, ey, depth)  with  A = -a/2 log2e, B = -b log2e, C = -c/2 log2e
   // so that z = A dx^2 + B dx dy + C dy^2 + log2 o = power * log2e + log2 o and alpha = min(0.99, 2^z).
-  // (ex, ey): half-extents of the ellipse where alpha >= 1/255 can hold (power >= -ln(255 o), minus a
-  // 1e-3 margin, +1% and +0.01 px): the blend skips whole 8x8 pixel blocks outside that box.
+  // (ex, ey): the alpha box (above).
   const float L2E = 1.4426950408889634f;
-  const float skip = -(log2x(255.0f * con.w) * 0.69314718055994531f) - 0.001f;
-  const float sq = -2.0f * skip;
-  const float ex = sq > 0.0f ? sqrtx(sq * ca) * 1.01f + 0.01f : -1.0f;
-  const float ey = sq > 0.0f ? sqrtx(sq * cc) * 1.01f + 0.01f : -1.0f;
   gs_st4<GS_NT_REC>(rec + 3 * o, make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E));
   gs_st4<GS_NT_REC>(rec + 3 * o + 1, make_float4(-0.5f * con.z * L2E, __log2f(con.w), cr, cg));
   gs_st4<GS_NT_REC>(rec + 3 * o + 2, make_float4(cbl, ex, ey, d));
@@ -1703,6 +1720,15 @@ __device__ const uint32_t* gs_spill_tile(const GsSpill& sp, uint32_t tx, uint32_
 //           before the Gaussian that would take T below 1e-4 (the reference's rule).
 // OVER (hybrid composite): per-pixel depth limit and an "under" image instead of the background colour
 template <bool OVER>
+#ifndef GS_EVAL_AB
+#define GS_EVAL_AB 0  // entries whose alphas are computed ahead of the transmittance chain (0: one at a time)
+#endif
+#ifndef GS_DONE_EVERY
+#define GS_DONE_EVERY 4u  // list entries between the wave's all-pixels-done tests (a power of two >= 4)
+#endif
+#ifndef GS_TERM_BRANCH
+#define GS_TERM_BRANCH 1  // the termination selects behind a wave-uniform branch (0: always applied)
+#endif
 #ifndef GS_BLEND_MIN_BLOCKS
 #define GS_BLEND_MIN_BLOCKS 8  // 64 VGPRs: 8 waves per SIMD (vs 7 at 70 VGPRs): +3% at C2
 #endif
@@ -2098,8 +2124,58 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const uint32_t cntu = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
     if (lane < 4) s_list[wave][cntu + lane] = GS_BLOCK * (uint32_t)sizeof(GStage);
     const uint32_t* list = s_list[wave];
+#if GS_EVAL_AB
+    // groups of GS_EVAL_AB entries: their records, quadratics and alphas first (independent: the
+    // reads and the exp2 chains overlap), then the transmittance chain through them in order (the only
+    // loop-carried dependency); the same operations as the one-entry form, so the image is identical
     for (uint32_t j = 0; j < cntu; j += 4) {
       if (__ballot(!done) == 0) break;
+      const uint4 o4 = *reinterpret_cast<const uint4*>(list + j);  // 4 list entries
+#pragma unroll
+      for (int h = 0; h < 4; h += GS_EVAL_AB) {
+        float al[GS_EVAL_AB], k0[GS_EVAL_AB], k1[GS_EVAL_AB], k2[GS_EVAL_AB];
+        bool behind[GS_EVAL_AB];
+#pragma unroll
+        for (int u = 0; u < GS_EVAL_AB; ++u) {
+          const int q = h + u;
+          const uint32_t o = q == 0 ? o4.x : q == 1 ? o4.y : q == 2 ? o4.z : o4.w;
+          const float4 a = *reinterpret_cast<const float4*>(stage + o);
+          const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
+          k2[u] = *reinterpret_cast<const float*>(stage + o + 32);
+          behind[u] = OVER && !(*reinterpret_cast<const float*>(stage + o + 44) < lim);
+          const float z = __builtin_fmaf(a.x, uxx, __builtin_fmaf(a.y, uxy, __builtin_fmaf(a.z, uyy,
+                                         __builtin_fmaf(a.w, ux, __builtin_fmaf(b.x, uy, b.y)))));
+          al[u] = z >= -7.9943534f ? fminf(0.99f, __builtin_amdgcn_exp2f(z)) : 0.0f;
+          k0[u] = b.z;
+          k1[u] = b.w;
+        }
+#pragma unroll
+        for (int u = 0; u < GS_EVAL_AB; ++u) {
+          if (OVER) done = done || behind[u];
+          const float alpha = done ? 0.0f : al[u];
+          float wgt = alpha * T;
+          float test_T = T - wgt;
+          const bool term = test_T < 0.0001f;
+#if GS_TERM_BRANCH
+          if (__ballot(term))
+#endif
+          {
+            done = done || term;
+            wgt = term ? 0.0f : wgt;
+            test_T = term ? T : test_T;
+          }
+          C0 = __builtin_fmaf(k0[u], wgt, C0);
+          C1 = __builtin_fmaf(k1[u], wgt, C1);
+          C2 = __builtin_fmaf(k2[u], wgt, C2);
+          T = test_T;
+        }
+      }
+    }
+#else
+    for (uint32_t j = 0; j < cntu; j += 4) {
+      // (the all-done test costs two VALU (the done mask from SGPRs to a compare): every
+      // GS_DONE_EVERY entries only)
+      if ((j & (GS_DONE_EVERY - 1u)) == 0u && __ballot(!done) == 0) break;
       const uint4 o4 = *reinterpret_cast<const uint4*>(list + j);  // 4 list entries
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -2125,7 +2201,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         float wgt = alpha * T;
         float test_T = T - wgt;
         const bool term = test_T < 0.0001f;  // only a valid pair can get there
-        if (__ballot(term)) {  // rare: this Gaussian would saturate the pixel -> stop before it
+#if GS_TERM_BRANCH
+        if (__ballot(term))  // rare: this Gaussian would saturate the pixel -> stop before it
+#endif
+        {
           done = done || term;
           wgt = term ? 0.0f : wgt;
           test_T = term ? T : test_T;
@@ -2136,6 +2215,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         T = test_T;
       }
     }
+#endif
   }
   STAMP(1, 2);
   if (fu.scap && tid == 0 && n_front) fu.cursor[tile] = 0;  // (n > 0: every wave passed a barrier after reading it)
@@ -2230,6 +2310,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   cam.row_end = std::min(tile_row_end, cam.grid_y);
   if (cam.row_end < cam.row_begin) cam.row_end = cam.row_begin;
   cam.cull = (g->chunk_bounds && (cam.row_begin > 0 || cam.row_end < cam.grid_y)) ? 1u : 0u;
+  cam.tight = (GS_TIGHT_BIN && !stats && !publish) ? 1u : 0u;
   const uint32_t tiles = cam.grid_x * cam.grid_y;
 
   if ((e = ensure(w->means2d, (size_t)n * 8))) return e;

@@ -223,7 +223,7 @@ def test_gaussians_over_capacity_frame_is_complete(native_lib, oracle_lib):
     from pathtracer_gaussiansplatting_amd import Renderer
     W, H = 256, 144
     g = Y.gaussians_c2(3000, seed=21)
-    g["scales"] *= 16.0  # K > 10 n: beyond the initial capacity
+    g["scales"] *= 24.0  # K > 10 n (also the alpha-box-binned K ~ 58k): beyond the initial capacity
     ubo = _gauss_ubo(W, H)
     ref = oracle_lib.splat_gaussians(g, ubo, W, H)
     assert ref["K"] > 10 * 3000, ref["K"]
@@ -234,13 +234,15 @@ def test_gaussians_over_capacity_frame_is_complete(native_lib, oracle_lib):
         r.splat_gaussians(dg, ubo, W, H, out)  # first frame: no stats, does not fit the pair buffer
         st = r.splat_status()
         assert st.frames == 0 and st.incomplete_tiles == 0, (st.frames, st.incomplete_tiles)
-        assert st.spilled_tiles > 0 and st.last_pairs == ref["K"] and st.pair_capacity < ref["K"]
+        # (the stream-ordered frame bins by the alpha box: at most the reference's K pairs)
+        k0 = st.last_pairs
+        assert st.spilled_tiles > 0 and st.pair_capacity < k0 <= ref["K"], (st.pair_capacity, k0, ref["K"])
         assert U.rel_l2(out.cpu().numpy(), ref["image"]) < 1e-4
         assert r.splat_status().spilled_tiles == 0  # read-and-clear
         out_b = torch.zeros_like(out)
         r.splat_gaussians(dg, ubo, W, H, out_b)  # grown from the published K: nothing spills
         st = r.splat_status()
-        assert st.frames == 0 and st.spilled_tiles == 0 and st.pair_capacity >= ref["K"]
+        assert st.frames == 0 and st.spilled_tiles == 0 and st.pair_capacity >= k0
         assert torch.equal(out_b, out)
         r2 = Renderer(0)  # with stats: the over-capacity attempt is re-run exactly inside the call
         try:
@@ -261,7 +263,7 @@ def test_gaussians_views_over_capacity_complete_per_view(native_lib, oracle_lib)
     from pathtracer_gaussiansplatting_amd import Renderer
     W, H = 256, 144
     g = Y.gaussians_c2(3000, seed=21)
-    g["scales"] *= 16.0
+    g["scales"] *= 24.0  # (alpha-box-binned K ~ 58k > the 10-per-Gaussian buffer)
     dg = {k: _dev(v) for k, v in g.items()}
     sc = U.cornell()
     ubos = [make_ubo(Camera(aspect=W / H).look_at([0.05 * k, 0.0, 0.0], [0.05 * k, 0.0, -1.0]), sc, 0)

@@ -312,3 +312,37 @@ def test_gaussians_tile_row_bands_with_chunk_bounds(native_lib, oracle_lib, radi
             assert torch.equal(comp, full), f"bands != full frame (frame {frame})"
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("shape", ["c2", "thin_faint"])
+def test_gaussians_alpha_box_binning_is_exact(native_lib, oracle_lib, shape):
+    """Timed (stream-ordered, unpublished, no stats) frames bin each Gaussian to the tiles its alpha
+    box overlaps instead of the reference's 3-sigma rectangle: fewer pairs, the same image bit for bit
+    (a pair outside the box has alpha < 1/255 at every pixel: the blend skips it exactly). Covered
+    with C2's Gaussians and with elongated, rotated, faint ones (opacities down to 1e-3, below the
+    1/255 cut: never binned) over a few camera positions."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H, n = 480, 270, 20_000
+    g = Y.gaussians_c2(n, seed=53)
+    if shape == "thin_faint":
+        rng = np.random.default_rng(7)
+        g["scales"] = (g["scales"] * rng.choice([0.05, 1.0, 4.0], size=(n, 3))).astype(np.float32)
+        g["opacities"] = rng.uniform(1e-3, 1.0, size=g["opacities"].shape).astype(np.float32) ** 3
+    ra = Renderer(0)
+    rb = Renderer(0, publish_splat_buffers=True)
+    try:
+        da = ra.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        db = {k: _dev(v) for k, v in g.items()}
+        for k, ubo in enumerate([orbit_ubo(j, W, H) for j in (0, 3)] + [orbit_ubo(6, W, H, radius=3.0)]):
+            for _ in range(2):  # three launches, then the fused front end
+                out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+                ra.splat_gaussians(da, ubo, W, H, out, bg=(0.1, 0.2, 0.3))
+                st = ra.splat_status()
+                assert st.frames == 0 and st.incomplete_tiles == 0
+                exact, ref = _exact(rb, db, ubo, W, H, oracle_lib, g, bg=(0.1, 0.2, 0.3))
+                assert torch.equal(out, exact), f"view {k}: box-binned frame != exact"
+                assert 0 < st.last_pairs < ref["K"], (st.last_pairs, ref["K"])
+            print(f"view {k}: pairs {st.last_pairs} of the reference's {ref['K']}")
+    finally:
+        ra.close()
+        rb.close()

@@ -38,10 +38,17 @@ def main():
     ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), cornell_box_scene(), 0)
     img = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
     r = Renderer(0, lib_path=lib)
+    if os.environ.get("GS_SORTED", "0") == "2":  # device Morton copy with ids (the bench's timed mode)
+        dg = r.sort_gaussians_spatial(dg)
+    rows = None
+    if os.environ.get("GS_BAND"):  # band k of 8 equal tile-row bands, with chunk bounds
+        k, gy = int(os.environ["GS_BAND"]), (H + 15) // 16
+        rows = (gy * k // 8, gy * (k + 1) // 8)
+        dg = dict(dg, chunk_bounds=r.gaussians_chunk_bounds(dg))
     for _ in range(5):  # (each finished before the next: the fused path starts once a frame has finished)
-        r.splat_gaussians(dg, ubo, W, H, img)
+        r.splat_gaussians(dg, ubo, W, H, img, tile_rows=rows)
         torch.cuda.synchronize()
-    r.splat_gaussians(dg, ubo, W, H, img)
+    r.splat_gaussians(dg, ubo, W, H, img, tile_rows=rows)
     torch.cuda.synchronize()
     st = r.splat_status()
     print(f"front end of the stamped frame: {'fused' if st.fused else 'three launches'} (touched runs {st.touched_runs})")
@@ -54,8 +61,11 @@ def main():
     assert dll.ptgs_debug_stamps(1, bs.ctypes.data, N8) == 0
     fe = os.environ.get("PTGS_GS_FRONTEND", "default")
     chunks = (n + 255) // 256  # GS_FUSED_THREADS Gaussians per fused workgroup
-    f = fs.reshape(-1, 8)[:chunks].astype(np.int64)
-    b = bs.reshape(-1, 8)[:120 * 68].astype(np.int64)
+    fall = fs.reshape(-1, 8).astype(np.int64)
+    f = fall[:chunks]
+    hlp = fall[chunks:chunks + 128]
+    nb = 120 * 68 if rows is None else 120 * (rows[1] - rows[0])
+    b = bs.reshape(-1, 8)[:nb].astype(np.int64)
     t0 = min(f[:, 0].min() if f[:, 0].any() else b[:, 0].min(), b[:, 0].min())
     print(f"n={n} sorted={os.environ.get('GS_SORTED', '0')} frontend={fe}")
     if st.fused:
@@ -68,6 +78,12 @@ def main():
             stats("  rect + barrier", f[:, 7] - f[:, 6])
             stats("  zero + scan + 2 barriers", f[:, 1] - f[:, 7])
         stats("workgroup total", f[:, 5] - f[:, 0])
+        print(f"  owner starts: first {0:.2f}, last {(f[:, 0].max() - f[:, 0].min()) * 0.01:.2f} us; "
+              f"ends: median {(np.median(f[:, 5]) - f[:, 0].min()) * 0.01:.2f}, last {(f[:, 5].max() - f[:, 0].min()) * 0.01:.2f} us")
+        hs = hlp[hlp[:, 0] > 0]
+        if len(hs):
+            print(f"  helpers: {len(hs)} stamped, starts {(hs[:, 0].min() - f[:, 0].min()) * 0.01:.2f} .. "
+                  f"{(hs[:, 0].max() - f[:, 0].min()) * 0.01:.2f} us")
         print(f"  gap fused end -> first blend start {(b[:, 0].min() - f[:, 5].max()) * 0.01:.2f} us")
     print(f"blend: {len(b)} workgroups, span {(b[:, 3].max() - b[:, 0].min()) * 0.01:.2f} us, "
           f"last start {(b[:, 0].max() - b[:, 0].min()) * 0.01:.2f} us after the first")
