@@ -20,6 +20,7 @@ def main():
     variants = sys.argv[1:] or ["base"]
     spp = int(os.environ.get("AB_SPP", "16"))
     rounds = int(os.environ.get("AB_ROUNDS", "3"))
+    calls = int(os.environ.get("AB_CALLS", "1"))  # consecutive calls per measurement (the viewer: AB_SPP=1 AB_CALLS=64)
     W, H = 1920, 1080
     scene = Y.atrium_scene(250_000, seed=2)
     scene.blue_noise = Y.blue_noise(1024)
@@ -38,11 +39,12 @@ def main():
     for rd in range(rounds + 1):
         for v in variants:
             r = rs[v]
-            ubo = make_ubo(pose, scene, 0, ambient=(0.3, 0.4, 0.5, 1.0), height=H)
+            ubos = [make_ubo(pose, scene, k * spp, ambient=(0.3, 0.4, 0.5, 1.0), height=H) for k in range(calls)]
             r.stats_reset()
             torch.cuda.synchronize()
             t = time.perf_counter()
-            r.trace_camera(ubo, W, H, acc, spp=spp)
+            for ubo in ubos:
+                r.trace_camera(ubo, W, H, acc, spp=spp)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t
             st = r.stats()
