@@ -1817,6 +1817,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     tile_x = tile - tile_y * cam.grid_x;
   }
 #endif
+  STAMP(1, 4);
   const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
   // Stage a record as the quadratic in tile-local pixel coordinates (ux, uy):
   // z = A ux^2 + B ux uy + C uy^2 + D ux + E uy + F (five FMAs per evaluation instead of seven), and
@@ -1854,6 +1855,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   }
   uint32_t n = range.y - range.x;
 #endif
+#ifdef GS_STAMP
+  if (tid == 0) __builtin_amdgcn_s_waitcnt(0);  // (the slot row and the count have arrived)
+  STAMP(1, 5);
+#endif
   const uint32_t n_front = n;  // (the front end's count: n becomes the completed count of a spilled tile)
   const bool small = slot_keys && n <= GS_BLOCK;
   if (fu.scap && tid == 0) fu.ranges[tile] = range;
@@ -1887,6 +1892,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
 #endif
     key = (k_cur & 0xFFFFFFFF00000000ull) | ((unsigned long long)g << 8) | tid;  // g < 2^24 (slot_keys)
   }
+#ifdef GS_STAMP
+  if (tid == 0 && small) {
+    __builtin_amdgcn_s_waitcnt(0);  // (wave 0's records have arrived)
+    STAMP(1, 6);
+  }
+#endif
   if (small) {
 #if GS_SMALL_RANK
    if (n <= GS_SMALL_RANK) {

@@ -90,6 +90,14 @@ def main():
     for k, nm in enumerate(["keys + sort + stage", "evaluation (wave 0)", "tail (slowest wave + store)"]):
         stats(nm, b[:, k + 1] - b[:, k])
     stats("workgroup total", b[:, 3] - b[:, 0])
+    sm = b[b[:, 6] > 0]  # small tiles: the dependent loads before the rank (wave 0 waited on each)
+    if len(sm):
+        print(f"  small tiles ({len(sm)}): keys + sort + stage split")
+        stats("  tile order load", sm[:, 4] - sm[:, 0])
+        stats("  slot row + count", sm[:, 5] - sm[:, 4])
+        stats("  records", sm[:, 6] - sm[:, 5])
+        stats("  rank + stage + barrier", sm[:, 1] - sm[:, 6])
+        stats("  evaluation", sm[:, 2] - sm[:, 1])
     # concurrency: workgroups resident over time
     ts = np.arange(b[:, 0].min(), b[:, 3].max(), 50)
     conc = [(np.count_nonzero((b[:, 0] <= t) & (b[:, 3] > t))) for t in ts]
