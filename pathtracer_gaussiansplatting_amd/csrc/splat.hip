@@ -76,8 +76,9 @@ struct SplatWorkspace {
   bool hint_recorded = false;
   hipEvent_t hint_event = nullptr;
   bool last_fused = false;    // the last frame ran the fused front end
-  uint32_t* k_host = nullptr;  // pinned, coherent [16]: K, largest tile, large tiles, skipped frames,
-                               // touched runs, fused overflow, publishing path (1 fused / 2 three)
+  uint32_t* k_host = nullptr;  // pinned, coherent [16]: K, largest tile, large tiles, -, touched runs,
+                               // fused overflow, publishing path (1 fused / 2 three), -, spill demand,
+                               // incomplete tile, bad ids, queued front-end slices
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
@@ -1796,6 +1797,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       const uint32_t used = min(fu.fz[GS_FSQ_W + 1], fu.fsq_cap);
       for (uint32_t k = tid; k < used; k += GS_BLOCK) fu.fsq[k] = make_uint2(0u, 0u);
       if (tid == 0) {
+        __atomic_store_n(fu.k_host + 11, fu.fz[GS_FSQ_W + 1], __ATOMIC_RELAXED);  // queued slices (helpers)
         fu.fz[GS_FSQ_W] = 0;
         fu.fz[GS_FSQ_W + 1] = 0;
         fu.fz[GS_FSQ_W + 2] = 0;
@@ -2554,8 +2556,19 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
       if ((e2 = ensure(w->cursor, (size_t)tiles * 4))) return e2;
       if ((e2 = hipMemsetAsync(w->cursor.p, 0, w->cursor.bytes, s))) return e2;
     }
-    // owners (bands x chunks) and helpers (bands x GS_FUSED_HELPERS) each publish their partials
-    const uint32_t nwg = nwg_fused + bgrid.bands * GS_FUSED_HELPERS;
+    // helper workgroups only when the latest fused frame queued slices (k_host[11]: a static view whose
+    // chunks all fit one slice launches none; the owners walk any slice no helper takes, so a frame
+    // that queues more than the helpers take is complete anyway). Idle helpers polled the queue until
+    // every owner had published, and their last poll (~3 us sleep) could end the kernel late.
+    static const int helpers_env = [] {
+      const char* v = getenv("PTGS_GS_HELPERS");  // "always" (A/B switch)
+      return v && !strcmp(v, "always") ? 1 : 0;
+    }();
+    const uint32_t queued = w->k_host[11];
+    const uint32_t helpers = helpers_env ? GS_FUSED_HELPERS
+                             : queued ? std::min<uint32_t>(GS_FUSED_HELPERS, queued + queued / 2u + 8u) : 0u;
+    // owners (bands x chunks) and helpers (bands x helpers) each publish their partials
+    const uint32_t nwg = nwg_fused + bgrid.bands * helpers;
     if ((e2 = ensure(w->fzp, (size_t)nwg * 8))) return e2;
     // slice queue: room for twice the slices of the largest pair count seen (+ one per owner); zero
     // once here, re-armed by the blend after every frame
@@ -2573,7 +2586,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     BinGrid fg = bgrid;
     fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
     fg.chunk = GS_FUSED_THREADS;
-    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks + GS_FUSED_HELPERS + (order ? 1u : 0u)),
+    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks + helpers + (order ? 1u : 0u)),
                        dim3(GS_FUSED_WG), band_lds, s,
                        cam, fpa, fg, scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
                        (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, order,
