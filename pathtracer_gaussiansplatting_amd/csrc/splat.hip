@@ -534,6 +534,14 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
 // ramp-down runs light tiles only. Any permutation renders the same image: the previous frame's
 // counts (ranges[t].y - .x, whatever path wrote them) only steer the schedule.
 #define GS_ORDER_BUCKETS 256u
+// order[b] = tile | (the previous frame's pair count of that tile, saturated) << GS_ORDER_TILE_BITS: the
+// blend loads only that much of the tile's key row with the tile (the rest, when the count grew, once
+// the count has arrived) instead of all 256 slots
+#define GS_ORDER_TILE_BITS 18u  // tiles < GS_MAX_GROUPS * 64 = 2^18
+#define GS_ORDER_HINT_MAX ((1u << (32u - GS_ORDER_TILE_BITS)) - 1u)
+#ifndef GS_ROW_HINT
+#define GS_ROW_HINT 1
+#endif
 __device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
   const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
   return GS_ORDER_BUCKETS - 1u - min(GS_ORDER_BUCKETS - 1u, n >> 1);
@@ -559,7 +567,11 @@ __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restri
   for (uint32_t t = tb + tid; t < te; t += nth) order[t - tb] = t;
   return;
 #endif
-  for (uint32_t t = tb + tid; t < te; t += nth) order[atomicAdd(s_h + gs_order_bucket(prev[t]), 1u)] = t;
+  for (uint32_t t = tb + tid; t < te; t += nth) {
+    const uint2 r = prev[t];
+    const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
+    order[atomicAdd(s_h + gs_order_bucket(r), 1u)] = t | (min(n, GS_ORDER_HINT_MAX) << GS_ORDER_TILE_BITS);
+  }
 }
 
 // Spill accounting (see gs_spill_tile), run by the first front-end launch's block (0, 0): the previous
@@ -1804,6 +1816,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       }
     }
   }
+  uint32_t row_hint = GS_BLOCK;  // slots of the key row loaded with the tile (the rest once n is known)
 #if GS_XCD_REMAP
   // XCD-aware: the workgroups of one XCD blend one horizontal strip of tiles, so the records of the
   // Gaussians they share stay in that XCD's L2
@@ -1813,8 +1826,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
 #else
   uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
   uint32_t tile = tile_y * cam.grid_x + tile_x;
-  if (fu.order) {  // fused frames: heavy tiles first (gs_tile_order)
-    tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)fu.order[blockIdx.y * gridDim.x + blockIdx.x]);
+  if (fu.order) {  // heavy tiles first (gs_tile_order)
+    const uint32_t ov = (uint32_t)__builtin_amdgcn_readfirstlane((int)fu.order[blockIdx.y * gridDim.x + blockIdx.x]);
+    tile = ov & ((1u << GS_ORDER_TILE_BITS) - 1u);
+#if GS_ROW_HINT
+    row_hint = min((uint32_t)GS_BLOCK, ((ov >> GS_ORDER_TILE_BITS) + 63u) & ~63u);
+#endif
     tile_y = tile / cam.grid_x;
     tile_x = tile - tile_y * cam.grid_x;
   }
@@ -1847,7 +1864,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   const unsigned long long k_slot = tid < n ? tile_slots[(size_t)tile * GS_TILE_SLOTS + tid] : ~0ull;
 #else
   const uint32_t srow = fu.scap ? fu.scap : GS_TILE_SLOTS;
-  const unsigned long long k_slot = tile_slots[(size_t)tile * srow + tid];
+  // (every work-item loads: those at or above the hint read the hint's last slot again, one line)
+  unsigned long long k_slot = tile_slots[(size_t)tile * srow + min(tid, max(row_hint, 1u) - 1u)];
   uint2 range;
   if (fu.scap) {
     const uint32_t c = fu.cursor[tile];
@@ -1856,6 +1874,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     range = ranges[tile];
   }
   uint32_t n = range.y - range.x;
+  if (tid >= row_hint && tid < n) k_slot = tile_slots[(size_t)tile * srow + tid];  // (the count grew)
 #endif
 #ifdef GS_STAMP
   if (tid == 0) __builtin_amdgcn_s_waitcnt(0);  // (the slot row and the count have arrived)
