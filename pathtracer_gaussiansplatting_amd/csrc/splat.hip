@@ -143,6 +143,7 @@ struct PreArgs {
                         // per-Gaussian outputs use it, so a reordered set renders like the original
   uint32_t* bad_ids;    // pinned host word set to 1 when an id is >= n (the Gaussian is dropped)
   const uint8_t* cskip;  // per 256-Gaussian chunk: 1 = its bound misses the frame's rows (gs_chunk_cull_kernel)
+  const float4* cbounds;  // the chunk bounds themselves (the fused front end tests its own chunk: no cull launch)
 };
 
 // Stores that may stream past L2 (A/B: GS_NT_REC for the blend records, GS_NT_OUT for the image)
@@ -873,6 +874,9 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
 // the per-workgroup chunk rects), so the frame is complete; the next frame sizes its rows from it.
 // fz: [1] largest tile above 256, [4] tiles above GS_MID pairs, [5] tiles above scap; per workgroup
 // fzp: (pairs, reservations); published to the host by the blend's block (0, 0).
+#ifndef GS_FUSED_OWN_CULL
+#define GS_FUSED_OWN_CULL 1  // a tile-row frame's fused workgroups test their chunk's bound (0: flags of a cull launch)
+#endif
 #ifndef GS_FUSED_THREADS
 #define GS_FUSED_THREADS 256  // Gaussians per fused workgroup (512 / 1 024 work-items: 1.5 us slower at C2)
 #endif
@@ -1075,7 +1079,11 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
     float d = 0.0f;  // view depth (every band's blocks need it for the keys; only band 0 stores it)
     // (tile-row shard with chunk bounds: a chunk whose bound misses the rows is skipped before its
     // Gaussians are loaded; it goes through the rest with no pairs)
+#if GS_FUSED_OWN_CULL
+    const bool skip = cam.cull && gs_chunk_misses(cam, A.cbounds[2 * chunk], A.cbounds[2 * chunk + 1]);
+#else
     const bool skip = cam.cull && A.cskip[chunk];
+#endif
     if (own && !skip) rc = store ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
     else if (own && store) gs_store_skipped(A, i);
     if (own && store) {  // for gs_spill_tile: the rect (empty: culled) and depth in walk order
@@ -2463,15 +2471,22 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   pa.ids = g->ids;
   pa.dbg_depths = (float*)w->dbg_depths.p;
   pa.bad_ids = w->k_dev + 10;
+  // chunks whose bound misses the rows are skipped by the front end before their loads: the fused
+  // kernel tests its own chunk's bound; the three-launch count reads flags of a small launch before it
   pa.cskip = nullptr;
-  if (cam.cull) {  // chunks whose bound misses the rows: skipped by the front end before their loads
+  pa.cbounds = cam.cull ? (const float4*)g->chunk_bounds : nullptr;
+  if (cam.cull) {
     const uint32_t nch = (n + 255u) / 256u;
     if ((e = ensure(w->cskip, nch))) return e;
-    hipLaunchKernelGGL(gs_chunk_cull_kernel, dim3((nch + 255u) / 256u), dim3(256), 0, s, cam,
-                       (const float4*)g->chunk_bounds, nch, (uint8_t*)w->cskip.p);
-    if ((e = hipGetLastError())) return e;
     pa.cskip = (const uint8_t*)w->cskip.p;
   }
+  auto cull_flags = [&]() -> hipError_t {
+    if (!cam.cull) return hipSuccess;
+    const uint32_t nch = (n + 255u) / 256u;
+    hipLaunchKernelGGL(gs_chunk_cull_kernel, dim3((nch + 255u) / 256u), dim3(256), 0, s, cam,
+                       (const float4*)g->chunk_bounds, nch, (uint8_t*)w->cskip.p);
+    return hipGetLastError();
+  };
   if (!publish) {  // the per-Gaussian debug outputs only for a published frame (ptgs_splat_get_buffers)
     pa.radii = nullptr;
     pa.touched = nullptr;
@@ -2599,6 +2614,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     const uint32_t fsq_cap = (uint32_t)std::min<size_t>(w->fsq.bytes / 8, 0x7FFFFFFFu);
     GsFused fu = {scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
                   (uint32_t*)w->fzp.p, nwg, order, (uint2*)w->fsq.p, fsq_cap};
+    if (!GS_FUSED_OWN_CULL && (e2 = cull_flags())) return e2;
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers (band 0 stores them for gs_spill_tile)
     fpa.rects = nullptr;
     fpa.depths = nullptr;
@@ -2685,6 +2701,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   auto enqueue_three = [&]() -> hipError_t {
     hipError_t e2;
     if ((e2 = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e2;
+    if ((e2 = cull_flags())) return e2;
     // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
     hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks + (order ? 1u : 0u)), dim3(GS_COUNT_THREADS),
                        std::max(band_lds, (size_t)GS_ORDER_BUCKETS * 4), s, cam, pa, bgrid, (uint32_t*)w->hist.p,

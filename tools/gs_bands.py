@@ -3,7 +3,7 @@
 GS_BANDS (default 8) equal tile-row bands, with and without ptgs_gaussians.chunk_bounds (per-rank chunk
 culling before the preprocess), against the full frame. One configuration per process so that a
 kernel trace (rocprofv3 --kernel-trace) separates the front end's kernels per configuration:
-   GS_CFG=c2|10m GS_BAND=full|<k> GS_BOUNDS=0|1 tools/gs_bands.py
+   GS_CFG=c2|10m GS_BAND=full|<k> GS_BOUNDS=0|1 [GS_LIB=libptgs_<variant>.so] tools/gs_bands.py
 Prints ms per frame (stream-ordered, steady state) and the frame's pairs."""
 import os
 import sys
@@ -24,7 +24,8 @@ def main():
     bounds = os.environ.get("GS_BOUNDS", "1") == "1"
     nb = int(os.environ.get("GS_BANDS", "8"))
     n, W, H, iters = CONFIGS[cfg]
-    r = Renderer(0)
+    lib = os.environ.get("GS_LIB", "libptgs.so")
+    r = Renderer(0, lib_path=lib if os.path.isabs(lib) else os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", lib))
     g = {k: torch.from_numpy(v).cuda() for k, v in Y.gaussians_c2(n, seed=1).items()}
     dg = r.sort_gaussians_spatial(g)
     del g
@@ -43,7 +44,7 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / iters
     st = r.splat_status()
-    print(f"{cfg} band {band}/{nb} rows {rows} bounds {int(bounds)}: {dt * 1e3:.4f} ms/frame, pairs {st.last_pairs}, "
+    print(f"{os.path.basename(lib)} {cfg} band {band}/{nb} rows {rows} bounds {int(bounds)}: {dt * 1e3:.4f} ms/frame, pairs {st.last_pairs}, "
           f"fused {st.fused}", flush=True)
     r.close()
 
