@@ -1750,6 +1750,9 @@ template <bool OVER>
 #ifndef GS_TERM_BRANCH
 #define GS_TERM_BRANCH 1  // the termination selects behind a wave-uniform branch (0: always applied)
 #endif
+#ifndef GS_FIRST_PLAIN
+#define GS_FIRST_PLAIN 1
+#endif
 #ifndef GS_BLEND_MIN_BLOCKS
 #define GS_BLEND_MIN_BLOCKS 8  // 64 VGPRs: 8 waves per SIMD (vs 7 at 70 VGPRs): +3% at C2
 #endif
@@ -2121,7 +2124,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   for (uint32_t base = 0; todo > 0; base += GS_BLOCK, todo -= GS_BLOCK) {
     // (small tiles: the barrier also publishes the records, masks and sorted slots staged after the
     // sort; large tiles: every wave is done with the previous batch)
+#if GS_FIRST_PLAIN
+    // (the first batch: done = !inside, and every tile holds a pixel inside the image: a plain barrier
+    // instead of the counting one, which reduces through LDS behind a second barrier)
+    if (base == 0) __syncthreads();
+    else if (__syncthreads_count(done) == GS_BLOCK) break;
+#else
     if (__syncthreads_count(done) == GS_BLOCK) break;
+#endif
     const uint32_t idx = base + tid;
     if (!small) {
       if (idx < n) {
