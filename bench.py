@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--no-hybrid", action="store_true")
     ap.add_argument("--no-gpu-bvh", action="store_true")
     ap.add_argument("--no-wavefront", action="store_true")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the timed C3 launch and C2 loop among the PT / 3DGS legs (no viewer, unsorted, "
+                         "views4, orbit legs): profiles/profile.sh, so that per-kernel averages are per-launch figures")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 Cornell-box leg")
     ap.add_argument("--no-torus", action="store_true", help="skip the torus data-collection leg (SURVEY 8f #1)")
     ap.add_argument("--no-capture", action="store_true", help="skip the dataset capture / export leg (SURVEY 8f #4)")
@@ -295,7 +298,7 @@ def main():
         # the viewer's protocol (recordCommandBuffer, engine.cpp:1971-1976): one sample per call at the
         # swapchain size, running mean of raygen_camera.rgen:80-87 into the accumulator, frame_count
         # advancing per call - SPP consecutive 1-spp calls against the one SPP-sample launch above
-        if world == 1:
+        if world == 1 and not args.headline_only:
             vacc = torch.zeros_like(accum)
             for k in range(4):
                 r.trace_camera(make_ubo(pose, scene, k, ambient=(0.3, 0.4, 0.5, 1.0), height=H), W, H, vacc, spp=1,
@@ -406,6 +409,7 @@ def main():
         c2_spilled = assert_complete(r, "C2 timed loop")
         # the same frames from the Gaussians in their generated (random) order: the same image bit for
         # bit, timed alone (secondary figure)
+        udt = None
         img0 = torch.zeros_like(img)
         r.splat_gaussians(dg0, gubo, W, H, img0, stream=stream)
         r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
@@ -413,47 +417,57 @@ def main():
         same_image = bool(torch.equal(img0, img))
         if not same_image:
             raise SystemExit("bench: the spatially ordered Gaussians render a different C2 frame")
-        for _ in range(3):
-            r.splat_gaussians(dg0, gubo, W, H, img0, stream=stream)
-        r.splat_status(stream)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(gsteps):
-            r.splat_gaussians(dg0, gubo, W, H, img0, stream=stream)
-        torch.cuda.synchronize()
-        udt = time.perf_counter() - t0
-        assert_complete(r, "C2 unsorted loop")
+        if not args.headline_only:
+            for _ in range(3):
+                r.splat_gaussians(dg0, gubo, W, H, img0, stream=stream)
+            r.splat_status(stream)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(gsteps):
+                r.splat_gaussians(dg0, gubo, W, H, img0, stream=stream)
+            torch.cuda.synchronize()
+            udt = time.perf_counter() - t0
+            assert_complete(r, "C2 unsorted loop")
         del img0
-        # per-stage split (separate, untimed pass: the stage events themselves cost ~40 us per frame)
+        # the reference's pair count (3-sigma rectangles: a frame with stats) beside the timed frames' own
+        # (alpha-box binning, published by every frame: ptgs_splat_status last_pairs)
+        st = r.splat_gaussians(dg, gubo, W, H, img, want_stats=True, stream=stream)
+        K_exact = int(st.num_rendered)
+        # per-stage split of the timed mode (separate, untimed pass: the stage events themselves cost ~40 us
+        # per frame; no stats, so the same frames as the timed loop)
         r.set_flags(FLAG_TIME_STAGES)
         stages = np.zeros(6)
+        for _ in range(3):
+            r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
         for _ in range(gsteps):
-            st = r.splat_gaussians(dg, gubo, W, H, img, want_stats=True, stream=stream)
+            r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
             stages += r.splat_stage_ms()
         r.set_flags(0)
         stages /= gsteps
+        gstat = r.splat_status(stream)
         N = args.gaussians
-        K = st.num_rendered
+        K = int(gstat.last_pairs)  # the timed frames' pairs
         P = math.ceil((32 + log2ceil(st.tiles_x * st.tiles_y)) / 8)
         b_gs = N * (56 + 48) + N * 48 + K * 12 + P * K * 24 + K * (4 + 48) + W * H * 16
         gms = gdt / gsteps * 1e3
         out["gs"] = {
             "value": round(N / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
             "workload": f"C2 3DGS forward: {N} synthetic Gaussians, {W}x{H}", "pairs_K": int(K),
+            "pairs_K_3sigma": K_exact,
             "skipped_frames": 0,  # incomplete frames: checked after every timed splat loop (ptgs_splat_status_read)
             "spilled_tiles": c2_spilled,
             "scaling": "strong", "parallelism": "single GPU" if world == 1 else
             f"tile-row shard x{world} (rows balanced by pair counts: {gs_rows}) + row gather to rank 0"
             + (" (ptgs_gather_rows, RCCL)" if native_comm else " (gloo rehearsal, host copies)"),
-            "front_end": "fused single launch" if st.fused else "count + colscan + scatter",
+            "front_end": "fused single launch" if gstat.fused else "count + colscan + scatter",
             "stages_ms": {k: round(float(v), 4) for k, v in
-                          zip(["front_end" if st.fused else "preprocess+count", "colscan", "scatter", "sort_large",
-                               "-", "sort_blend"], stages) if k != "-" and not (st.fused and k in ("colscan", "scatter"))},
+                          zip(["front_end" if gstat.fused else "preprocess+count", "colscan", "scatter", "sort_large",
+                               "-", "sort_blend"], stages) if k != "-" and not (gstat.fused and k in ("colscan", "scatter"))},
             "gaussian_order": f"3D Morton order of the means (ptgs_gaussians_sort_spatial, {prep_ms:.2f} ms once, "
                               "untimed scene preparation; identical image to the generated order, checked)",
-            "unsorted_order": {"value": round(N / (udt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
-                               "ms_per_step": round(udt / gsteps * 1e3, 4),
-                               "note": "the same frames from the Gaussians in their generated (random) order"},
+            "unsorted_order": None if udt is None else {
+                "value": round(N / (udt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(udt / gsteps * 1e3, 4),
+                "note": "the same frames from the Gaussians in their generated (random) order"},
             "roofline": {"bound": "hbm", "kernel": "whole pipeline", "achieved": round(b_gs / (gms * 1e-3) / 1e9, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(b_gs / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "alg_bytes": b_gs},
@@ -471,7 +485,7 @@ def main():
             "alg_bytes_per_launch": b_alg,
             "note": "algorithmic: 8-B key + 48-B blend record per (Gaussian, tile) pair + 16 B per pixel"})
         out["gs"]["splat_pairs_per_s"] = round(K / (gdt / gsteps) / 1e9, 4)  # (Gaussian, tile) instances, G/s
-        if world == 1:
+        if world == 1 and not args.headline_only:
             # four views of the C2 Gaussians per call (ptgs_splat_gaussians_views: forked streams, one
             # workspace per view), the capture-loop use: aggregate Gaussians x views per second
             vubos = [make_ubo(Camera(aspect=W / H).look_at([0.25 * k, 0.0, 0.0], [0.25 * k, 0.0, -1.0]),

@@ -186,18 +186,9 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   // walk, at i) and radii / touched / means2d / conic (ptgs_splat_get_buffers) when their pointers are
   // set (the fused path without PTGS_FLAG_SPLAT_PUBLISH leaves them out)
   const uint32_t o = A.ids ? A.ids[i] : i;
-  if (STORE && rects) rects[i] = none;  // empty rect: the scatter reads rects only
-  if (o >= A.n) {  // ids must be a permutation of [0, n): an index outside it is dropped, not written
-    if (STORE) __atomic_store_n(A.bad_ids, 1u, __ATOMIC_RELAXED);  // (reported by the next call)
-    return none;
-  }
-  if (STORE && radii) {
-    radii[o] = 0;
-    touched[o] = 0;
-  }
+  // every input is loaded here, with the id and before the id check and the depth test: one memory round
+  // trip per Gaussian (loads behind either branch were issued only once the id / the means had arrived)
   float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
-  // every input is loaded here, before the depth test: one memory round trip per Gaussian (loads
-  // behind the test's branch were issued only once the means had arrived)
   float qr = rots[4 * i], qx = rots[4 * i + 1], qy = rots[4 * i + 2], qz = rots[4 * i + 3];
   float sx = scales[3 * i], sy = scales[3 * i + 1], sz = scales[3 * i + 2];
   float op = opac[i];
@@ -208,8 +199,18 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
     cbl = colors[3 * i + 2];
     asm volatile("" : "+v"(cr), "+v"(cg), "+v"(cbl));
   }
-  // (the empty asm needs the values here, so the compiler cannot sink the loads behind the branch)
-  asm volatile("" : "+v"(qr), "+v"(qx), "+v"(qy), "+v"(qz), "+v"(sx), "+v"(sy), "+v"(sz), "+v"(op));
+  // (the empty asm needs the values here, so the compiler cannot sink the loads behind the branches)
+  asm volatile("" : "+v"(mx), "+v"(my), "+v"(mz), "+v"(qr), "+v"(qx), "+v"(qy), "+v"(qz), "+v"(sx), "+v"(sy),
+               "+v"(sz), "+v"(op));
+  if (STORE && rects) rects[i] = none;  // empty rect: the scatter reads rects only
+  if (o >= A.n) {  // ids must be a permutation of [0, n): an index outside it is dropped, not written
+    if (STORE) __atomic_store_n(A.bad_ids, 1u, __ATOMIC_RELAXED);  // (reported by the next call)
+    return none;
+  }
+  if (STORE && radii) {
+    radii[o] = 0;
+    touched[o] = 0;
+  }
   // frustum: view-space depth d = -z (RH, camera looks down -Z)
   v4 pv = mv4(cam.view, mx, my, mz, 1.0f);
   float d = -pv.z;
@@ -541,7 +542,7 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
 #define GS_ORDER_TILE_BITS 18u  // tiles < GS_MAX_GROUPS * 64 = 2^18
 #define GS_ORDER_HINT_MAX ((1u << (32u - GS_ORDER_TILE_BITS)) - 1u)
 #ifndef GS_ROW_HINT
-#define GS_ROW_HINT 1
+#define GS_ROW_HINT 0  // measured slower: C2 0.0594 vs 0.0588 ms without the hint (tools/gs_ab.sh, 3 rounds)
 #endif
 __device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
   const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
@@ -875,7 +876,10 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
 // fz: [1] largest tile above 256, [4] tiles above GS_MID pairs, [5] tiles above scap; per workgroup
 // fzp: (pairs, reservations); published to the host by the blend's block (0, 0).
 #ifndef GS_FUSED_OWN_CULL
-#define GS_FUSED_OWN_CULL 1  // a tile-row frame's fused workgroups test their chunk's bound (0: flags of a cull launch)
+// a tile-row frame of at most this many chunks: the fused workgroups test their own chunk's bound (no
+// cull launch: C2 bands 1-2 us faster); above it the flags of a cull launch (each workgroup's bound
+// test adds its latency to every round of workgroups: 10M at 4K, band 0 2.26 vs 2.09 ms)
+#define GS_FUSED_OWN_CULL 1024u
 #endif
 #ifndef GS_FUSED_THREADS
 #define GS_FUSED_THREADS 256  // Gaussians per fused workgroup (512 / 1 024 work-items: 1.5 us slower at C2)
@@ -1079,11 +1083,8 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
     float d = 0.0f;  // view depth (every band's blocks need it for the keys; only band 0 stores it)
     // (tile-row shard with chunk bounds: a chunk whose bound misses the rows is skipped before its
     // Gaussians are loaded; it goes through the rest with no pairs)
-#if GS_FUSED_OWN_CULL
-    const bool skip = cam.cull && gs_chunk_misses(cam, A.cbounds[2 * chunk], A.cbounds[2 * chunk + 1]);
-#else
-    const bool skip = cam.cull && A.cskip[chunk];
-#endif
+    const bool skip = cam.cull && (A.cbounds ? gs_chunk_misses(cam, A.cbounds[2 * chunk], A.cbounds[2 * chunk + 1])
+                                             : A.cskip[chunk] != 0);
     if (own && !skip) rc = store ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
     else if (own && store) gs_store_skipped(A, i);
     if (own && store) {  // for gs_spill_tile: the rect (empty: culled) and depth in walk order
@@ -2624,8 +2625,11 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     const uint32_t fsq_cap = (uint32_t)std::min<size_t>(w->fsq.bytes / 8, 0x7FFFFFFFu);
     GsFused fu = {scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
                   (uint32_t*)w->fzp.p, nwg, order, (uint2*)w->fsq.p, fsq_cap};
-    if (!GS_FUSED_OWN_CULL && (e2 = cull_flags())) return e2;
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers (band 0 stores them for gs_spill_tile)
+    if (cam.cull && (n + 255u) / 256u > GS_FUSED_OWN_CULL) {
+      if ((e2 = cull_flags())) return e2;
+      fpa.cbounds = nullptr;
+    }
     fpa.rects = nullptr;
     fpa.depths = nullptr;
     BinGrid fg = bgrid;

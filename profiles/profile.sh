@@ -11,7 +11,7 @@ set -euo pipefail
 TAG=${1:-r02}
 # only the headline legs (C3 path trace, C2 splat): every dispatch of a kernel is the same workload,
 # so the per-kernel averages are the per-launch figures bench.py reports
-ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-hybrid --no-gs-1m --no-gs-10m --no-gpu-bvh --no-c1 --no-c5 --no-torus --no-capture"}
+ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --headline-only --no-cpu-baseline --no-hybrid --no-gs-1m --no-gs-10m --no-gpu-bvh --no-c1 --no-c5 --no-torus --no-capture"}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
