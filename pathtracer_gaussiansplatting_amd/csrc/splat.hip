@@ -2235,8 +2235,22 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
 #endif
         const uint32_t o = u == 0 ? o4.x : u == 1 ? o4.y : u == 2 ? o4.z : o4.w;
         const float4 a = *reinterpret_cast<const float4*>(stage + o);
+#ifdef GS_PROBE_LDS_A  // (timing probe: one LDS read per entry instead of three; wrong image, and its
+                       // coefficients end pixels early: not a clean measure of the LDS reads)
+        const float4 b = make_float4(a.w, a.z, a.y, a.x);
+        const float cb = a.y;
+#else
         const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
         const float cb = *reinterpret_cast<const float*>(stage + o + 32);
+#endif
+#ifdef GS_PROBE_LDS_X2  // (timing probe: 16 of a record's 36 B read twice from LDS, the copy only waited for: same image)
+        {
+          uint32_t z0 = 0;
+          asm volatile("" : "+v"(z0));
+          const float4 a2 = *reinterpret_cast<const float4*>(stage + (o ^ z0) + 16);
+          asm volatile("" ::"v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w));
+        }
+#endif
         if (OVER) {  // sorted by depth: the first Gaussian at or behind the mesh ends the pixel
           const float gd = *reinterpret_cast<const float*>(stage + o + 44);
           done = done || !(gd < lim);
