@@ -109,10 +109,15 @@ def test_gaussians_timed_c2_mode_vs_oracle(native_lib, oracle_lib):
     try:
         dg = ra.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
         outs = []
-        for _ in range(4):  # frame 0: three launches; 1..3: fused, steady state
+        for k in range(4):  # frame 0: three launches; 1..3: fused, steady state
             out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
             ra.splat_gaussians(dg, ubo, W, H, out)
             outs.append(out)
+            if k == 0:
+                # the row sizes reach the host once frame 0 has run (a finished frame's hint, never
+                # waited for by the call): without this wait a fast host enqueues every frame before
+                # frame 0 has finished, and they all take the three-launch path
+                torch.cuda.synchronize()
         st = ra.splat_status()
         assert st.fused == 1 and st.frames == 0 and st.spilled_tiles == 0, (st.fused, st.frames, st.spilled_tiles)
         exact, ref = _exact(rb, {k: _dev(v) for k, v in g.items()}, ubo, W, H, oracle_lib, g)
