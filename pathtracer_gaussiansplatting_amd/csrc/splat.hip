@@ -1754,6 +1754,9 @@ template <bool OVER>
 #ifndef GS_FIRST_PLAIN
 #define GS_FIRST_PLAIN 1
 #endif
+#ifndef GS_EXACT_Q
+#define GS_EXACT_Q 1  // exact quadrant test at staging: C2 0.0585 -> 0.0577 ms, bit-exact (C2, 1M)
+#endif
 #ifndef GS_BLEND_MIN_BLOCKS
 #define GS_BLEND_MIN_BLOCKS 8  // 64 VGPRs: 8 waves per SIMD (vs 7 at 70 VGPRs): +3% at C2
 #endif
@@ -1866,8 +1869,38 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const float x0 = gx - gc.y, x1 = gx + gc.y, y0 = gy - gc.z, y1 = gy + gc.z;
     const bool xl = x0 <= 7.0f && x1 >= 0.0f, xr = x0 <= 15.0f && x1 >= 8.0f;
     const bool yt = y0 <= 7.0f && y1 >= 0.0f, yb = y0 <= 15.0f && y1 >= 8.0f;
-    return (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
-           ((uint32_t)(xr && yb) << 3);
+    uint32_t qm = (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
+                  ((uint32_t)(xr && yb) << 3);
+#if GS_EXACT_Q
+    // exact quadrant test: the largest z over a quadrant's pixel square (z concave: A, C < 0) is at the
+    // centre when the centre lies inside, else on an edge, each edge's a clamped 1D parabola. A quadrant
+    // whose largest z is below log2(1/255) (minus a 0.02 margin for the rounding of the staged form)
+    // has no pixel with alpha >= 1/255: the entry would be evaluated to nothing by every lane of its wave.
+    {
+      // the vertex u* = -q / (2p) = q * (-1 / (2p)) (an approximate reciprocal: the value at a point near
+      // the vertex is within the margin of the maximum)
+      const float i2a = -0.5f * __builtin_amdgcn_rcpf(A), i2c = -0.5f * __builtin_amdgcn_rcpf(C);
+      auto vmax = [](float p, float q, float r, float inv, float u0, float u1) {
+        const float u = fminf(fmaxf(q * inv, u0), u1);
+        return __builtin_fmaf(__builtin_fmaf(p, u, q), u, r);
+      };
+      const float zk = -7.9943534f - 0.02f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo_x = (q & 1) ? 8.0f : 0.0f, lo_y = (q >> 1) ? 8.0f : 0.0f;
+        const float hi_x = lo_x + 7.0f, hi_y = lo_y + 7.0f;
+        const bool inside = gx >= lo_x && gx <= hi_x && gy >= lo_y && gy <= hi_y;
+        // x = lo_x / hi_x over y in [lo_y, hi_y]; y = lo_y / hi_y over x in [lo_x, hi_x]
+        const float m0 = vmax(C, __builtin_fmaf(B, lo_x, E), __builtin_fmaf(__builtin_fmaf(A, lo_x, D), lo_x, F), i2c, lo_y, hi_y);
+        const float m1 = vmax(C, __builtin_fmaf(B, hi_x, E), __builtin_fmaf(__builtin_fmaf(A, hi_x, D), hi_x, F), i2c, lo_y, hi_y);
+        const float m2 = vmax(A, __builtin_fmaf(B, lo_y, D), __builtin_fmaf(__builtin_fmaf(C, lo_y, E), lo_y, F), i2a, lo_x, hi_x);
+        const float m3 = vmax(A, __builtin_fmaf(B, hi_y, D), __builtin_fmaf(__builtin_fmaf(C, hi_y, E), hi_y, F), i2a, lo_x, hi_x);
+        const float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+        if (!inside && !(m >= zk)) qm &= ~(1u << q);
+      }
+    }
+#endif
+    return qm;
   };
   // the tile's slot row is loaded together with its range (no dependent round trip for small tiles)
 #ifdef GS_PROBE_SLOT_N
