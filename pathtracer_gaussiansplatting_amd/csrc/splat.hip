@@ -1859,7 +1859,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   // in tile-local coordinates against the quadrants' pixel ranges [0, 7] / [8, 15] (immediates: no
   // register holds a tile bound across the batch loop; the box's 1% + 0.01 px margin covers the
   // rounding of the local shift). (An exact ellipse-vs-block refinement measured slower on C2.)
-  auto stage_rec = [&](uint32_t slot, const float4& ga, const float4& gb, const float4& gc) -> uint32_t {
+  auto stage_rec = [&](uint32_t slot, const float4& ga, const float4& gb, const float4& gc, bool exact = true) -> uint32_t {
     const float gx = ga.x - tx0, gy = ga.y - ty0, A = ga.z, B = ga.w, C = gb.x;
     const float D = -2.0f * A * gx - B * gy, E = -B * gx - 2.0f * C * gy;
     const float F = ((A * gx * gx + B * gx * gy) + C * gy * gy) + gb.y;
@@ -1872,6 +1872,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     uint32_t qm = (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
                   ((uint32_t)(xr && yb) << 3);
 #if GS_EXACT_Q
+    if (exact)
     // exact quadrant test: the largest z over a quadrant's pixel square (z concave: A, C < 0) is at the
     // centre when the centre lies inside, else on an edge, each edge's a clamped 1D parabola. A quadrant
     // whose largest z is below log2(1/255) (minus a 0.02 margin for the rounding of the staged form)
@@ -2169,7 +2170,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const uint32_t idx = base + tid;
     if (!small) {
       if (idx < n) {
-        s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
+        s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, false);  // (large tiles: the box test only)
       }
       // next batch: its records (values loaded a batch ago) and the values of the one after
       if (idx + GS_BLOCK < n) {
