@@ -1754,6 +1754,9 @@ template <bool OVER>
 #ifndef GS_FIRST_PLAIN
 #define GS_FIRST_PLAIN 1
 #endif
+#ifndef GS_EVAL_RFL
+#define GS_EVAL_RFL 0
+#endif
 #ifndef GS_EXACT_Q
 #define GS_EXACT_Q 1  // exact quadrant test at staging: C2 0.0585 -> 0.0577 ms, bit-exact (C2, 1M)
 #endif
@@ -2268,8 +2271,25 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         if (u == 2) __builtin_amdgcn_sched_barrier(0);
 #endif
         const uint32_t o = u == 0 ? o4.x : u == 1 ? o4.y : u == 2 ? o4.z : o4.w;
+#if GS_EVAL_RFL
+        // one lane reads the record (the LDS returns 36 B instead of 64 x 36 B) and the values reach the
+        // wave as scalar operands through readfirstlane
+        float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = a1;
+        float c1 = 0.0f;
+        if (lane == 0) {
+          a1 = *reinterpret_cast<const float4*>(stage + o);
+          b1 = *reinterpret_cast<const float4*>(stage + o + 16);
+          c1 = *reinterpret_cast<const float*>(stage + o + 32);
+        }
+        auto rfl = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+        const float4 a = make_float4(rfl(a1.x), rfl(a1.y), rfl(a1.z), rfl(a1.w));
+        const float4 b = make_float4(rfl(b1.x), rfl(b1.y), rfl(b1.z), rfl(b1.w));
+        const float cb = rfl(c1);
+#else
         const float4 a = *reinterpret_cast<const float4*>(stage + o);
-#ifdef GS_PROBE_LDS_A  // (timing probe: one LDS read per entry instead of three; wrong image, and its
+#endif
+#if GS_EVAL_RFL
+#elif defined(GS_PROBE_LDS_A)  // (timing probe: one LDS read per entry instead of three; wrong image, and its
                        // coefficients end pixels early: not a clean measure of the LDS reads)
         const float4 b = make_float4(a.w, a.z, a.y, a.x);
         const float cb = a.y;
@@ -2277,7 +2297,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
         const float cb = *reinterpret_cast<const float*>(stage + o + 32);
 #endif
-#ifdef GS_PROBE_LDS_X2  // (timing probe: 16 of a record's 36 B read twice from LDS, the copy only waited for: same image)
+#if defined(GS_PROBE_LDS_X2) && !GS_EVAL_RFL  // (timing probe: 16 of a record's 36 B read twice from LDS, the copy only waited for: same image)
         {
           uint32_t z0 = 0;
           asm volatile("" : "+v"(z0));
