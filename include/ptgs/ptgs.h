@@ -45,8 +45,11 @@ extern "C" {
 #define PTGS_EINCOMPLETE (-6) /* an EARLIER stream-ordered splat frame of this context could not be completed
                                * (its spill pool was exhausted: some tiles were left at the background).
                                * Returned once, by the first splat call that starts after that frame has
-                               * finished on the device; that call has grown the pool and rendered its own
-                               * frame completely. ptgs_splat_reserve prevents it (see there). */
+                               * finished on the device; that call has grown the pool to 1.25x the latest
+                               * pair count published (which bounds the reported frame's spilled pairs) and
+                               * rendered its own frame completely unless its own spilled tiles need more.
+                               * ptgs_splat_gaussians_views renders every view before it returns the code.
+                               * ptgs_splat_reserve prevents it (see there). */
 
 /* ---------------- reference struct layouts (Appendix B of SURVEY.md) ---------------- */
 
@@ -171,6 +174,102 @@ typedef struct ptgs_ray_push {
     float minor_radius;
     float height;
 } ptgs_ray_push;
+
+/* Layout contract: every size / offset of the structs above against Helpers/GeneralHeaders.h (glm's
+ * vec3 is 12 B, vec4 16 B with no over-alignment on the host: GeneralHeaders.h:65-97 Vertex, :236-269
+ * MaterialPushConstant, :287-297 PunctualLight, :300-318 UniformBufferObject, :515-540 MeshInfo /
+ * RaySample / RayPushConstant / PC, :565-576 HitDataGPU, :594-609 LightTriangle / LightCDF /
+ * PunctualLightCDF). Any translation unit that includes this header (the library's C++ sources, a C
+ * caller, tests/native/abi_layout.c) fails to compile on a drift. */
+#if defined(__cplusplus)
+#define PTGS_LAYOUT_ASSERT(cond, msg) static_assert(cond, msg)
+#else
+#define PTGS_LAYOUT_ASSERT(cond, msg) _Static_assert(cond, msg)
+#endif
+#define PTGS_AT(T, f, off) PTGS_LAYOUT_ASSERT(offsetof(T, f) == (off), #T "." #f " at " #off)
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_vertex) == 80, "Vertex is 80 B");
+PTGS_AT(ptgs_vertex, pos, 0);
+PTGS_AT(ptgs_vertex, pad1, 12);
+PTGS_AT(ptgs_vertex, normal, 16);
+PTGS_AT(ptgs_vertex, pad2, 28);
+PTGS_AT(ptgs_vertex, color, 32);
+PTGS_AT(ptgs_vertex, pad3, 44);
+PTGS_AT(ptgs_vertex, tangent, 48);
+PTGS_AT(ptgs_vertex, tex_coord, 64);
+PTGS_AT(ptgs_vertex, tex_coord_1, 72);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_material) == 308, "MaterialPushConstant is 308 B");
+PTGS_AT(ptgs_material, base_color_factor, 0);
+PTGS_AT(ptgs_material, uv_normal, 16);
+PTGS_AT(ptgs_material, uv_emissive, 80);
+PTGS_AT(ptgs_material, uv_albedo, 144);
+PTGS_AT(ptgs_material, emissive_factor_and_pad, 208);
+PTGS_AT(ptgs_material, metallic_factor, 224);
+PTGS_AT(ptgs_material, roughness_factor, 228);
+PTGS_AT(ptgs_material, occlusion_strength, 232);
+PTGS_AT(ptgs_material, specular_factor, 236);
+PTGS_AT(ptgs_material, specular_color_factor, 240);
+PTGS_AT(ptgs_material, alpha_cutoff, 252);
+PTGS_AT(ptgs_material, transmission_factor, 256);
+PTGS_AT(ptgs_material, clearcoat_factor, 260);
+PTGS_AT(ptgs_material, clearcoat_roughness_factor, 264);
+PTGS_AT(ptgs_material, pad, 268);
+PTGS_AT(ptgs_material, albedo_texture_index, 272);
+PTGS_AT(ptgs_material, normal_texture_index, 276);
+PTGS_AT(ptgs_material, metallic_roughness_texture_index, 280);
+PTGS_AT(ptgs_material, emissive_texture_index, 284);
+PTGS_AT(ptgs_material, occlusion_texture_index, 288);
+PTGS_AT(ptgs_material, clearcoat_texture_index, 292);
+PTGS_AT(ptgs_material, clearcoat_roughness_texture_index, 296);
+PTGS_AT(ptgs_material, sg_id, 300);
+PTGS_AT(ptgs_material, use_specular_glossiness_workflow, 304);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_ubo) == 192, "UniformBufferObject is 192 B");
+PTGS_AT(ptgs_ubo, view, 0);
+PTGS_AT(ptgs_ubo, proj, 64);
+PTGS_AT(ptgs_ubo, camera_pos, 128);
+PTGS_AT(ptgs_ubo, frame_count, 140);
+PTGS_AT(ptgs_ubo, ambient_light, 144);
+PTGS_AT(ptgs_ubo, emissive_flux, 160);
+PTGS_AT(ptgs_ubo, punctual_flux, 164);
+PTGS_AT(ptgs_ubo, total_flux, 168);
+PTGS_AT(ptgs_ubo, p_emissive, 172);
+PTGS_AT(ptgs_ubo, fov, 176);
+PTGS_AT(ptgs_ubo, height, 180);
+PTGS_AT(ptgs_ubo, use_lod, 184);
+PTGS_AT(ptgs_ubo, lod_factor, 188);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_punctual_light) == 64, "PunctualLight is 64 B");
+PTGS_AT(ptgs_punctual_light, position, 0);
+PTGS_AT(ptgs_punctual_light, intensity, 12);
+PTGS_AT(ptgs_punctual_light, color, 16);
+PTGS_AT(ptgs_punctual_light, range, 28);
+PTGS_AT(ptgs_punctual_light, direction, 32);
+PTGS_AT(ptgs_punctual_light, outer_cone_cos, 44);
+PTGS_AT(ptgs_punctual_light, inner_cone_cos, 48);
+PTGS_AT(ptgs_punctual_light, type, 52);
+PTGS_AT(ptgs_punctual_light, padding, 56);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_mesh_info) == 16, "MeshInfo is 16 B");
+PTGS_AT(ptgs_mesh_info, material_index, 0);
+PTGS_AT(ptgs_mesh_info, vertex_offset, 4);
+PTGS_AT(ptgs_mesh_info, index_offset, 8);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_light_triangle) == 16, "LightTriangle is 16 B");
+PTGS_AT(ptgs_light_triangle, material_index, 12);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_light_cdf) == 16, "LightCDF is 16 B");
+PTGS_AT(ptgs_light_cdf, triangle_index, 4);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_punctual_cdf) == 16, "PunctualLightCDF is 16 B");
+PTGS_AT(ptgs_punctual_cdf, light_index, 4);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_hitdata) == 48, "HitDataGPU is 48 B");
+PTGS_AT(ptgs_hitdata, pos, 0);
+PTGS_AT(ptgs_hitdata, flag, 12);
+PTGS_AT(ptgs_hitdata, color, 16);
+PTGS_AT(ptgs_hitdata, normal, 32);
+PTGS_AT(ptgs_hitdata, padding, 44);
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_ray_sample) == 8, "RaySample is 8 B");
+PTGS_LAYOUT_ASSERT(sizeof(ptgs_ray_push) == 80, "RayPushConstant / PC is 80 B");
+PTGS_AT(ptgs_ray_push, model, 0);
+PTGS_AT(ptgs_ray_push, mode, 64);
+PTGS_AT(ptgs_ray_push, major_radius, 68);
+PTGS_AT(ptgs_ray_push, minor_radius, 72);
+PTGS_AT(ptgs_ray_push, height, 76);
+#undef PTGS_AT
 
 /* ---------------- scene ---------------- */
 

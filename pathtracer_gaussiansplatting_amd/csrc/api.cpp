@@ -625,9 +625,13 @@ int ptgs_synchronize(ptgs_ctx* c) {
 
 extern "C" {
 
-static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
+// Renders one frame; PTGS_OK means it was enqueued completely. *report (bit 0: an earlier frame was left
+// incomplete, bit 1: an earlier frame met ids >= count) is about EARLIER frames of the workspace: the
+// caller turns it into PTGS_EINCOMPLETE / PTGS_EINVAL (splat_report) once everything it renders is enqueued.
+static int splat_render(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
                         const float bg[3], const float* depth, const float* under, uint32_t tile_row_begin,
-                        uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream) {
+                        uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream, uint32_t* report) {
+  *report = 0;
   if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
   if (g->count && (!is_device_ptr(g->means) || !is_device_ptr(g->scales) || !is_device_ptr(g->rotations) ||
                    !is_device_ptr(g->opacities) || !is_device_ptr(g->colors) || (g->ids && !is_device_ptr(g->ids))))
@@ -639,16 +643,28 @@ static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
   HIPCHK(c, hipSetDevice(c->device));
   float mvp[16];
   mat4_mul(ubo->proj, ubo->view, mvp);
-  uint32_t report = 0;
   hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, depth, under,
                                  tile_row_begin, tile_row_end, out, stats, (c->flags & PTGS_FLAG_TIME_STAGES) != 0,
-                                 (c->flags & PTGS_FLAG_SPLAT_PUBLISH) != 0, (hipStream_t)stream, &report);
+                                 (c->flags & PTGS_FLAG_SPLAT_PUBLISH) != 0, (hipStream_t)stream, report);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_gaussians: %s", hipGetErrorString(e));
-  // (this frame is rendered; the codes report an earlier frame of the workspace)
+  return PTGS_OK;
+}
+
+// (the frames of this call are rendered; the codes report earlier frames of the workspace(s))
+static int splat_report(ptgs_ctx* c, uint32_t report) {
   if (report & 2u) return fail(c, PTGS_EINVAL, "an earlier splat frame met ptgs_gaussians.ids entries >= count");
   if (report & 1u)
     return fail(c, PTGS_EINCOMPLETE, "an earlier splat frame left tiles incomplete (spill pool exhausted; grown)");
   return PTGS_OK;
+}
+
+static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
+                        const float bg[3], const float* depth, const float* under, uint32_t tile_row_begin,
+                        uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream) {
+  uint32_t report = 0;
+  const int rc = splat_render(c, g, ubo, w, h, bg, depth, under, tile_row_begin, tile_row_end, out, stats, stream,
+                              &report);
+  return rc != PTGS_OK ? rc : splat_report(c, report);
 }
 
 int ptgs_splat_gaussians(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
@@ -694,6 +710,7 @@ int ptgs_splat_gaussians_views(ptgs_ctx* c, const ptgs_gaussians* g, uint32_t n_
   // on any failure after a view was forked, the views already launched are joined back into the
   // caller's stream before returning (later work there must not race them)
   uint32_t launched = 1;
+  uint32_t report = 0;  // the views' reports about their earlier frames (PTGS_EINCOMPLETE / PTGS_EINVAL)
   auto join = [&]() {
     for (uint32_t v = 1; v < launched; ++v) (void)hipStreamWaitEvent(s, c->view_join[v], 0);
   };
@@ -702,17 +719,21 @@ int ptgs_splat_gaussians_views(ptgs_ctx* c, const ptgs_gaussians* g, uint32_t n_
     if (e != hipSuccess) { join(); return fail(c, PTGS_EHIP, "hipStreamWaitEvent: %s", hipGetErrorString(e)); }
     SplatWorkspace* keep = c->splat;
     c->splat = c->view_ws[v];
-    const int rc = splat_common(c, g, &ubos[v], w, h, bg, nullptr, nullptr, 0, ~0u, outs[v], nullptr, c->view_stream[v]);
+    uint32_t rep = 0;
+    const int rc = splat_render(c, g, &ubos[v], w, h, bg, nullptr, nullptr, 0, ~0u, outs[v], nullptr, c->view_stream[v],
+                                &rep);
     c->splat = keep;
+    report |= rep;  // (about earlier frames of view v's workspace: returned once every view is enqueued)
     // (record the join even after a failed view: kernels it did enqueue must be waited for)
     e = hipEventRecord(c->view_join[v], c->view_stream[v]);
     if (e == hipSuccess) launched = v + 1;
     if (rc != PTGS_OK) { join(); return rc; }
     if (e != hipSuccess) { join(); return fail(c, PTGS_EHIP, "hipEventRecord: %s", hipGetErrorString(e)); }
   }
-  const int rc = splat_common(c, g, &ubos[0], w, h, bg, nullptr, nullptr, 0, ~0u, outs[0], nullptr, stream);
+  uint32_t rep = 0;
+  const int rc = splat_render(c, g, &ubos[0], w, h, bg, nullptr, nullptr, 0, ~0u, outs[0], nullptr, stream, &rep);
   join();
-  return rc;
+  return rc != PTGS_OK ? rc : splat_report(c, report | rep);
 }
 
 int ptgs_gaussians_sort_spatial(ptgs_ctx* c, const ptgs_gaussians* g, float* means, float* scales, float* rotations,

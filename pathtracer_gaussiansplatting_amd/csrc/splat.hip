@@ -27,21 +27,14 @@
 
 #include "../../include/ptgs/ptgs.h"
 #include "detmath.h"
-#include "xcd.h"
 #include "splat.h"
+#include "splat_probe.h"
 
 namespace ptgs {
 
-#ifndef GS_XCD_REMAP
-#define GS_XCD_REMAP 0
-#endif
 #define GS_BLOCK_X 16
 #define GS_BLOCK_Y 16
 #define GS_BLOCK (GS_BLOCK_X * GS_BLOCK_Y)
-
-#ifndef GS_TIGHT_BIN
-#define GS_TIGHT_BIN 1  // timed frames bin by the alpha box (SplatCam::tight)
-#endif
 
 struct SplatCam {
   float view[16];
@@ -146,22 +139,12 @@ struct PreArgs {
   const float4* cbounds;  // the chunk bounds themselves (the fused front end tests its own chunk: no cull launch)
 };
 
-// Stores that may stream past L2 (A/B: GS_NT_REC for the blend records, GS_NT_OUT for the image)
-template <bool NT>
-__device__ __forceinline__ void gs_st4(float4* p, const float4& v) {
+// Image stores stream past L2 (non-temporal): C2 0.0686 -> 0.0677 ms, fewer dirty lines at the kernel end.
+// (Non-temporal blend records and key rows measured slower: the blend reads both right after.)
+__device__ __forceinline__ void gs_st4_nt(float4* p, const float4& v) {
   typedef float f4v __attribute__((ext_vector_type(4)));
-  if (NT) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
-  else *p = v;
+  __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
 }
-#ifndef GS_NT_REC
-#define GS_NT_REC 0
-#endif
-#ifndef GS_NT_OUT
-#define GS_NT_OUT 1  // image stores stream out: C2 0.0686 -> 0.0677 ms (fewer dirty lines at the kernel end)
-#endif
-#ifndef GS_NT_SLOTS
-#define GS_NT_SLOTS 0
-#endif
 
 // One Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T, EWA Sigma' = J W Sigma W^T J^T + 0.3,
 // conic, 3-sigma radius, tile rect (returned; empty if culled) and, with STORE, every per-Gaussian
@@ -311,9 +294,9 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   // so that z = A dx^2 + B dx dy + C dy^2 + log2 o = power * log2e + log2 o and alpha = min(0.99, 2^z).
   // (ex, ey): the alpha box (above).
   const float L2E = 1.4426950408889634f;
-  gs_st4<GS_NT_REC>(rec + 3 * o, make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E));
-  gs_st4<GS_NT_REC>(rec + 3 * o + 1, make_float4(-0.5f * con.z * L2E, __log2f(con.w), cr, cg));
-  gs_st4<GS_NT_REC>(rec + 3 * o + 2, make_float4(cbl, ex, ey, d));
+  rec[3 * o] = make_float4(pimg.x, pimg.y, -0.5f * con.x * L2E, -con.y * L2E);
+  rec[3 * o + 1] = make_float4(-0.5f * con.z * L2E, __log2f(con.w), cr, cg);
+  rec[3 * o + 2] = make_float4(cbl, ex, ey, d);
   return rect;
 }
 
@@ -473,9 +456,6 @@ __device__ __forceinline__ void gs_clip(const ushort4& rc, uint32_t ty0, uint32_
 // each wave first filters (64 rects per step, GS_WALK_PF steps in flight; ballot + mbcnt append the
 // hits to its GS_WQ-entry LDS ring) and expands 64 queued entries at a time (depths gathered then).
 #define GS_WQ 128
-#ifndef GS_SCATTER_DIRECT
-#define GS_SCATTER_DIRECT 1  // one band (1080p): direct walk, -0.4 us at C2 (kernel trace)
-#endif
 #define GS_WALK_PF 4
 template <typename F>
 __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* __restrict__ rects,
@@ -536,14 +516,8 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
 // ramp-down runs light tiles only. Any permutation renders the same image: the previous frame's
 // counts (ranges[t].y - .x, whatever path wrote them) only steer the schedule.
 #define GS_ORDER_BUCKETS 256u
-// order[b] = tile | (the previous frame's pair count of that tile, saturated) << GS_ORDER_TILE_BITS: the
-// blend loads only that much of the tile's key row with the tile (the rest, when the count grew, once
-// the count has arrived) instead of all 256 slots
-#define GS_ORDER_TILE_BITS 18u  // tiles < GS_MAX_GROUPS * 64 = 2^18
-#define GS_ORDER_HINT_MAX ((1u << (32u - GS_ORDER_TILE_BITS)) - 1u)
-#ifndef GS_ROW_HINT
-#define GS_ROW_HINT 0  // measured slower: C2 0.0594 vs 0.0588 ms without the hint (tools/gs_ab.sh, 3 rounds)
-#endif
+// (order[b] = the tile. Carrying the previous frame's count of the tile in the word, so the blend loads
+// only that much of the key row with the tile, measured slower: C2 0.0594 vs 0.0588 ms)
 __device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
   const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
   return GS_ORDER_BUCKETS - 1u - min(GS_ORDER_BUCKETS - 1u, n >> 1);
@@ -565,15 +539,7 @@ __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restri
     s_h[4 * lane + 3] = ex + c0 + c1 + c2;
   }
   __syncthreads();
-#ifdef GS_ORDER_IDENTITY  // (A/B probe: the blend's extra load without the reordering)
-  for (uint32_t t = tb + tid; t < te; t += nth) order[t - tb] = t;
-  return;
-#endif
-  for (uint32_t t = tb + tid; t < te; t += nth) {
-    const uint2 r = prev[t];
-    const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
-    order[atomicAdd(s_h + gs_order_bucket(r), 1u)] = t | (min(n, GS_ORDER_HINT_MAX) << GS_ORDER_TILE_BITS);
-  }
+  for (uint32_t t = tb + tid; t < te; t += nth) order[atomicAdd(s_h + gs_order_bucket(prev[t]), 1u)] = t;
 }
 
 // Spill accounting (see gs_spill_tile), run by the first front-end launch's block (0, 0): the previous
@@ -663,12 +629,10 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
       by0 = min(by0, yh & 0xFFFFu);
       by1 = max(by1, (yh & 0xFFFFu) + (yh >> 16));
     }
-#ifndef GS_PROBE_NO_WALK
     if (__ballot(yh != 0u))
       gs_expand<false>(lane, i, xw, yh, 0.0f, [&](uint32_t, uint32_t x, uint32_t y, float) {
         atomicAdd(s_hist + (y - ty0) * bg.grid_x + x, 1u);
       });
-#endif
   }
   __syncthreads();
   uint32_t* row = hist + (size_t)blockIdx.y * bg.tiles + ty0 * bg.grid_x;
@@ -826,9 +790,6 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     if (c == 0) ranges[t] = ti.y ? make_uint2(start, start + ti.y) : make_uint2(0u, 0u);
   }
   __syncthreads();
-#ifdef GS_PROBE_NO_WALK
-  return;
-#endif
   auto put = [&](uint32_t i, uint32_t x, uint32_t y, float d) {
     const unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | i;
     const uint32_t k = (y - ty0) * bg.grid_x + x;
@@ -840,8 +801,8 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
       tile_slots[dst + rel] = key;
     }
   };
-#if GS_SCATTER_DIRECT
-  if (bg.bands == 1) {  // one band: every rect meets it, so no filtering ring (one Gaussian per lane, as the count)
+  if (bg.bands == 1) {  // one band: every rect meets it, so no filtering ring (one Gaussian per lane, as the count;
+                        // -0.4 us at C2, kernel trace)
     const uint32_t b0 = c * bg.chunk, b1 = min(n, b0 + bg.chunk);
     for (uint32_t base = b0 + wv * 64u; base < b1; base += GS_BIN_THREADS) {
       const uint32_t i = base + lane;
@@ -857,7 +818,6 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     }
     return;
   }
-#endif
   gs_walk_chunk(bg, rects, depths, ids, n, ty0, ty1, s_q, put);
 }
 
@@ -896,23 +856,6 @@ struct GsFused {  // the sort's and the blend's view of a fused-front-end frame 
   uint2* fsq;             // the front end's slice queue (re-armed by block (0, 0): entries and fz[12..14])
   uint32_t fsq_cap;
 };
-// GS_STAMP builds (tools/gs_stamps.py): per-workgroup s_memrealtime (100 MHz) stamps at phase
-// boundaries of the fused front end and the blend, read back with ptgs_debug_stamps.
-#ifdef GS_STAMP
-#define GS_STAMP_WG 65536
-#define GS_STAMP_N 8
-__device__ unsigned long long g_gs_stamps[2][GS_STAMP_WG * GS_STAMP_N];
-#define STAMP(kind, k)                                                                                      \
-  do {                                                                                                     \
-    const uint32_t wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                              \
-    if (threadIdx.x == 0 && wg_ < GS_STAMP_WG)                                                             \
-      g_gs_stamps[kind][wg_ * GS_STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime();                       \
-  } while (0)
-#define STAMP_SYNC() __syncthreads()
-#else
-#define STAMP(kind, k) do { } while (0)
-#define STAMP_SYNC() do { } while (0)
-#endif
 #ifndef GS_FUSED_WG
 #define GS_FUSED_WG 512  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
 #endif
@@ -929,9 +872,6 @@ __device__ unsigned long long g_gs_stamps[2][GS_STAMP_WG * GS_STAMP_N];
 // Returns the work-item's pair count.
 #ifndef GS_FUSED_QREG
 #define GS_FUSED_QREG 8  // pairs per work-item of a slice (GS_FUSED_SLICE / GS_FUSED_WG; C2 needs <= 7)
-#endif
-#ifndef GS_FUSED_KEEP
-#define GS_FUSED_KEEP 1
 #endif
 #define GS_KEEP_RB (GS_FUSED_THREADS <= 256 ? 8u : 9u)  // bits of rank and of j (< GS_FUSED_THREADS)
 static_assert(GS_FUSED_THREADS <= 512 && GS_BAND_TILES <= 8192, "gs_wg_count_keep's packing");
@@ -997,6 +937,10 @@ __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, con
 #define GS_FUSED_WAVES 6  // waves per SIMD (3 workgroups of 512 work-items per CU; 8 forces SGPR spills)
 #endif
 static_assert(GS_FUSED_SLICE <= (uint32_t)GS_FUSED_WG * GS_FUSED_QREG, "a slice's pairs are kept in registers");
+// chunk skip flags (cskip) and chunk bounds are per 256 Gaussians (ptgs_gaussians_chunk_bounds): the fused
+// workgroups index them by their own chunk, so a fused chunk must be exactly that
+static_assert(GS_FUSED_THREADS == 256, "the fused chunk is the chunk-bounds granule (256 Gaussians)");
+
 
 __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                          uint32_t scap,
@@ -1034,7 +978,9 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
   {  // helpers claim one queued slice (one per helper: no loop keeps the camera's registers live)
     if (!owner) {
       if (threadIdx.x == 0) {
-        uint32_t job = 0xFFFFFFFFu, hidx = 0, spins = 0;
+        // (owner, slice) in two words: an owner index is bands x chunks, beyond any packing's bits at 8K
+        // with tens of millions of Gaussians
+        uint32_t job = 0xFFFFFFFFu, jslice = 0, hidx = 0, spins = 0;
         for (;;) {
           if (!hidx) hidx = atomicAdd(fz + GS_FSQ_W, 1u) + 1u;  // (1-based: 0 = none claimed)
           const uint32_t idx = hidx - 1u;
@@ -1054,11 +1000,13 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
           }
           hidx = 0;  // this index is settled: the next iteration claims another
           if (v != GS_FSQ_TAKEN && atomicCAS(&fsq[idx].x, v, GS_FSQ_TAKEN) == v) {
-            job = ((v - 1u) << 12) | (uint32_t)(ev >> 32);
+            job = v - 1u;
+            jslice = (uint32_t)(ev >> 32);
             break;
           }
         }
         s_job[0] = job;
+        s_job[3] = jslice;
       }
       __syncthreads();
       const uint32_t job = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_job[0]);
@@ -1070,8 +1018,8 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
         }
         return;
       }
-      wg = job >> 12;
-      slice = job & 0xFFFu;
+      wg = job;
+      slice = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_job[3]);
     }
     const uint32_t band = wg % gridDim.x, chunk = wg / gridDim.x;
     const uint32_t ty0 = band * bg.band_rows, ty1 = min(bg.grid_y, ty0 + bg.band_rows);
@@ -1091,10 +1039,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
       rects_out[i] = rc;
       depths_out[i] = d;
     }
-#ifdef GS_STAMP
-    if (threadIdx.x == 0) __builtin_amdgcn_s_waitcnt(0);  // (wave 0's preprocess, loads included)
-    STAMP(0, 6);
-#endif
+    STAMP_WAITED(0, 6);  // (wave 0's preprocess, loads included)
     uint32_t xw, yh;
     gs_clip(rc, ty0, ty1, xw, yh);
     // the chunk's bounding tile rect (within the band): the LDS histogram covers only it, so zeroing
@@ -1227,9 +1172,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
           const uint32_t t = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
           if (rel < scap) {
             const unsigned long long key = ((unsigned long long)e.w << 32) | e.z;
-            unsigned long long* dst = tile_slots + (size_t)t * scap + rel;
-            if (GS_NT_SLOTS) __builtin_nontemporal_store(key, dst);
-            else *dst = key;
+            tile_slots[(size_t)t * scap + rel] = key;
           }
         }
       }
@@ -1277,10 +1220,8 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
     fzp[2 * fw] = p;
     fzp[2 * fw + 1] = r;
   }
-#ifdef GS_STAMP
   STAMP_SYNC();
   STAMP(0, 5);
-#endif
 }
 
 // ascending bitonic sort ("flip" network: every comparator puts the min at the lower index) over
@@ -1384,9 +1325,6 @@ __device__ __forceinline__ uint32_t gs_radix_tile(uint32_t* dep0, uint32_t* dep1
   const uint32_t p0 = tid * R, p1 = min(n, p0 + R);  // this work-item's positions
   uint32_t cur = 0;
   for (uint32_t sh = 0; sh < nbits; sh += 4) {
-#ifdef GS_PROBE_SORT_PASSES
-    if (sh >= 4 * GS_PROBE_SORT_PASSES) continue;
-#endif
     const uint32_t* sd = cur ? dep1 : dep0;
     const uint16_t* ss = cur ? slot1 : slot0;
     uint32_t* dd = cur ? dep0 : dep1;
@@ -1609,15 +1547,7 @@ __device__ __forceinline__ uint32_t gs_run_below(const unsigned long long* b, un
 #ifndef GS_MERGE_MIN
 #define GS_MERGE_MIN 96u  // (counting is cheaper for up to ~1.5 runs)
 #endif
-#ifndef GS_RANK_MERGE
-#define GS_RANK_MERGE 1
-#endif
 #define GS_ARENA (48 * (GS_BLOCK + 1) + 4 * (GS_BLOCK + 4) * 4)  // staged records + per-quadrant lists
-#ifndef GS_SMALL_RANK
-// small tiles of at most this many pairs are ranked by counting instead of sorted by the register
-// bitonic network: blend 70.6 -> 68.1 us at C2 (kernel trace; 128: 67.8, within noise)
-#define GS_SMALL_RANK 256
-#endif
 
 struct GStage {  // one staged blend record (see gs_preprocess_one)
   float4 a, b, c;
@@ -1649,6 +1579,7 @@ struct GsSpill {
 };
 #define GS_SPILL_LDS 1984u  // keys sorted in the blend's LDS arena (15 872 B + the candidate list + counters)
 #define GS_SPILL_CAND 128u  // front-end workgroups tested per round
+static_assert(GS_ARENA >= 8u * GS_SPILL_LDS + 4u * (GS_SPILL_CAND + 3u), "gs_spill_tile's keys, candidates and counters fit the arena");
 
 // Returns the sorted gaussians of tile (tx, ty) in the pool and their count in m (on entry: the
 // tile's pair count), or nullptr when the pool is exhausted. Uses the arena (>= 16 400 B of LDS).
@@ -1726,43 +1657,32 @@ __device__ const uint32_t* gs_spill_tile(const GsSpill& sp, uint32_t tx, uint32_
 // dispatcher's dynamic balancing, 103 vs 72 us at C2; a tile-pair workgroup shading two pixels per
 // lane in packed f32 measured 133 vs 104 us per frame: the per-pixel done / valid bookkeeping of the
 // pair and the strip lists cost more than the packing saved).
-//  sort     tiles of <= 256 pairs: one key per work-item, ranked by counting against all n keys in
-//           LDS (GS_SMALL_RANK; the register bitonic network remains for a smaller limit); while it
-//           runs, the blend records of the unsorted keys are already in flight, and the staging slot
-//           of sorted position r is recorded; then publish the sorted keys (tile << 32 | depth) /
-//           values (gaussian). Larger tiles were sorted and published by gs_sort_large_kernel: their values
+//  sort     tiles of <= 256 pairs: one key per work-item; up to GS_MERGE_MIN pairs ranked by counting
+//           against all n keys in LDS, above that by merge ranking (gs_wave_sort64 + gs_run_below);
+//           while it runs, the blend records of the unsorted keys are already in flight, and the
+//           staging slot of sorted position r is recorded; then publish the sorted keys (tile << 32 |
+//           depth) / values (gaussian). Tiles of (256, GS_MID] pairs are merge-ranked two keys per
+//           work-item. Larger tiles were sorted and published by gs_sort_large_kernel: their values
 //           are streamed in batches of 256, the records of batch b + 1 (and the values of b + 2) in
 //           flight while batch b blends.
 //  blend    wave w shades the 8x8 quadrant q = w of the tile (x half w & 1, y half w >> 1), one pixel
 //           per lane. Each staged Gaussian's alpha box is tested against the four quadrants (a 4-bit
-//           mask in LDS); every wave ballots bit w over the batch's masks in sorted order into its own
-//           list (no cross-wave counts: one barrier per batch), so a wave iterates only the
-//           Gaussians that can touch its 64 pixels. alpha = min(0.99, 2^z) with the hardware exp2
-//           (within 1e-4 relative L2 of the oracle's exp, test_raster_gpu.py); front to back, stop
-//           before the Gaussian that would take T below 1e-4 (the reference's rule).
+//           mask in LDS; small tiles add the exact per-quadrant test, stage_rec); every wave ballots
+//           bit w over the batch's masks in sorted order into its own list (no cross-wave counts: one
+//           barrier per batch), so a wave iterates only the Gaussians that can touch its 64 pixels.
+//           alpha = min(0.99, 2^z) with the hardware exp2 (within 1e-4 relative L2 of the oracle's exp,
+//           test_raster_gpu.py); front to back, stop before the Gaussian that would take T below 1e-4
+//           (the reference's rule).
 // OVER (hybrid composite): per-pixel depth limit and an "under" image instead of the background colour
-template <bool OVER>
-#ifndef GS_EVAL_AB
-#define GS_EVAL_AB 0  // entries whose alphas are computed ahead of the transmittance chain (0: one at a time)
-#endif
-#ifndef GS_DONE_EVERY
+// Measured and rejected here (git history: round 4): records read by one lane and broadcast with
+// readfirstlane (C2 0.0784 vs 0.0565 ms), alphas of several entries computed ahead of the transmittance
+// chain, the termination applied without its wave-uniform branch, an XCD-aware tile mapping, loading the
+// key row only up to the previous frame's count, non-temporal records / key rows.
 #define GS_DONE_EVERY 4u  // list entries between the wave's all-pixels-done tests (a power of two >= 4)
-#endif
-#ifndef GS_TERM_BRANCH
-#define GS_TERM_BRANCH 1  // the termination selects behind a wave-uniform branch (0: always applied)
-#endif
-#ifndef GS_FIRST_PLAIN
-#define GS_FIRST_PLAIN 1
-#endif
-#ifndef GS_EVAL_RFL
-#define GS_EVAL_RFL 0
-#endif
-#ifndef GS_EXACT_Q
-#define GS_EXACT_Q 1  // exact quadrant test at staging: C2 0.0585 -> 0.0577 ms, bit-exact (C2, 1M)
-#endif
 #ifndef GS_BLEND_MIN_BLOCKS
 #define GS_BLEND_MIN_BLOCKS 8  // 64 VGPRs: 8 waves per SIMD (vs 7 at 70 VGPRs): +3% at C2
 #endif
+template <bool OVER>
 __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_kernel(SplatCam cam, const uint2* __restrict__ ranges,
                                                                  unsigned long long* __restrict__ pairs,
                                                                  uint32_t sorted_above,
@@ -1780,8 +1700,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   __shared__ __attribute__((aligned(16))) char s_arena[GS_ARENA];
   GStage* s_stage = reinterpret_cast<GStage*>(s_arena);
   uint32_t(*s_list)[GS_BLOCK + 4] = reinterpret_cast<uint32_t(*)[GS_BLOCK + 4]>(s_arena + sizeof(GStage) * (GS_BLOCK + 1));
-  // the register sort's 64 / 128 exchanges and a mid tile's ranked keys alias the arena: records are
-  // staged only after the last read of either (behind a barrier)
+  // the merge ranks' sorted runs and a mid tile's ranked keys alias the arena: records are staged only
+  // after the last read of either (behind a barrier)
   unsigned long long* s_key = reinterpret_cast<unsigned long long*>(s_arena);
   __shared__ uint8_t s_mask[GS_BLOCK];
   __shared__ uint8_t s_sslot[GS_BLOCK];  // small tiles: staging slot of sorted position p
@@ -1834,26 +1754,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       }
     }
   }
-  uint32_t row_hint = GS_BLOCK;  // slots of the key row loaded with the tile (the rest once n is known)
-#if GS_XCD_REMAP
-  // XCD-aware: the workgroups of one XCD blend one horizontal strip of tiles, so the records of the
-  // Gaussians they share stay in that XCD's L2
-  const uint32_t tl = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  const uint32_t tile_x = tl % gridDim.x, tile_y = cam.row_begin + tl / gridDim.x;
-  const uint32_t tile = tile_y * cam.grid_x + tile_x;
-#else
   uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
   uint32_t tile = tile_y * cam.grid_x + tile_x;
   if (fu.order) {  // heavy tiles first (gs_tile_order)
-    const uint32_t ov = (uint32_t)__builtin_amdgcn_readfirstlane((int)fu.order[blockIdx.y * gridDim.x + blockIdx.x]);
-    tile = ov & ((1u << GS_ORDER_TILE_BITS) - 1u);
-#if GS_ROW_HINT
-    row_hint = min((uint32_t)GS_BLOCK, ((ov >> GS_ORDER_TILE_BITS) + 63u) & ~63u);
-#endif
+    tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)fu.order[blockIdx.y * gridDim.x + blockIdx.x]);
     tile_y = tile / cam.grid_x;
     tile_x = tile - tile_y * cam.grid_x;
   }
-#endif
   STAMP(1, 4);
   const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
   // Stage a record as the quadratic in tile-local pixel coordinates (ux, uy):
@@ -1861,8 +1768,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   // return the quadrant mask of its alpha box: bit q = (x half q & 1, y half q >> 1), the box tested
   // in tile-local coordinates against the quadrants' pixel ranges [0, 7] / [8, 15] (immediates: no
   // register holds a tile bound across the batch loop; the box's 1% + 0.01 px margin covers the
-  // rounding of the local shift). (An exact ellipse-vs-block refinement measured slower on C2.)
-  auto stage_rec = [&](uint32_t slot, const float4& ga, const float4& gb, const float4& gc, bool exact = true) -> uint32_t {
+  // rounding of the local shift). exact: also the exact quadrant test (small tiles; the large-tile batch
+  // loop keeps the box test: its copy of the test spilled 2 VGPRs).
+  auto stage_rec = [&](uint32_t slot, const float4& ga, const float4& gb, const float4& gc, bool exact) -> uint32_t {
     const float gx = ga.x - tx0, gy = ga.y - ty0, A = ga.z, B = ga.w, C = gb.x;
     const float D = -2.0f * A * gx - B * gy, E = -B * gx - 2.0f * C * gy;
     const float F = ((A * gx * gx + B * gx * gy) + C * gy * gy) + gb.y;
@@ -1874,13 +1782,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const bool yt = y0 <= 7.0f && y1 >= 0.0f, yb = y0 <= 15.0f && y1 >= 8.0f;
     uint32_t qm = (uint32_t)(xl && yt) | ((uint32_t)(xr && yt) << 1) | ((uint32_t)(xl && yb) << 2) |
                   ((uint32_t)(xr && yb) << 3);
-#if GS_EXACT_Q
-    if (exact)
-    // exact quadrant test: the largest z over a quadrant's pixel square (z concave: A, C < 0) is at the
-    // centre when the centre lies inside, else on an edge, each edge's a clamped 1D parabola. A quadrant
-    // whose largest z is below log2(1/255) (minus a 0.02 margin for the rounding of the staged form)
-    // has no pixel with alpha >= 1/255: the entry would be evaluated to nothing by every lane of its wave.
-    {
+    if (exact) {
+      // exact quadrant test (C2 0.0585 -> 0.0577 ms, bit-exact): the largest z over a quadrant's pixel
+      // square (z concave: A, C < 0) is at the centre when the centre lies inside, else on an edge, each
+      // edge's a clamped 1D parabola. A quadrant whose largest z is below log2(1/255) (minus a 0.02
+      // margin for the rounding of the staged form) has no pixel with alpha >= 1/255: the entry would be
+      // evaluated to nothing by every lane of its wave.
       // the vertex u* = -q / (2p) = q * (-1 / (2p)) (an approximate reciprocal: the value at a point near
       // the vertex is within the margin of the maximum)
       const float i2a = -0.5f * __builtin_amdgcn_rcpf(A), i2c = -0.5f * __builtin_amdgcn_rcpf(C);
@@ -1903,18 +1810,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         if (!inside && !(m >= zk)) qm &= ~(1u << q);
       }
     }
-#endif
     return qm;
   };
-  // the tile's slot row is loaded together with its range (no dependent round trip for small tiles)
-#ifdef GS_PROBE_SLOT_N
-  const uint2 range = ranges[tile];
-  const uint32_t n = range.y - range.x;
-  const unsigned long long k_slot = tid < n ? tile_slots[(size_t)tile * GS_TILE_SLOTS + tid] : ~0ull;
-#else
+  // the tile's slot row is loaded together with its count (no dependent round trip for small tiles;
+  // every work-item loads its slot whatever the count)
   const uint32_t srow = fu.scap ? fu.scap : GS_TILE_SLOTS;
-  // (every work-item loads: those at or above the hint read the hint's last slot again, one line)
-  unsigned long long k_slot = tile_slots[(size_t)tile * srow + min(tid, max(row_hint, 1u) - 1u)];
+  const unsigned long long k_slot = tile_slots[(size_t)tile * srow + tid];
   uint2 range;
   if (fu.scap) {
     const uint32_t c = fu.cursor[tile];
@@ -1923,12 +1824,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     range = ranges[tile];
   }
   uint32_t n = range.y - range.x;
-  if (tid >= row_hint && tid < n) k_slot = tile_slots[(size_t)tile * srow + tid];  // (the count grew)
-#endif
-#ifdef GS_STAMP
-  if (tid == 0) __builtin_amdgcn_s_waitcnt(0);  // (the slot row and the count have arrived)
-  STAMP(1, 5);
-#endif
+  STAMP_WAITED(1, 5);  // (the slot row and the count have arrived)
   const uint32_t n_front = n;  // (the front end's count: n becomes the completed count of a spilled tile)
   const bool small = slot_keys && n <= GS_BLOCK;
   if (fu.scap && tid == 0) fu.ranges[tile] = range;
@@ -1953,29 +1849,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   if (small && tid < n) {
     const unsigned long long k_cur = k_slot;
     const uint32_t g = (uint32_t)k_cur;
-#ifdef GS_PROBE_NO_REC
-    ra = rb = rc = make_float4((float)g, 0.f, 0.f, 0.f);
-#else
-    ra = rec[3 * g];
-    rb = rec[3 * g + 1];
-    rc = rec[3 * g + 2];
-#endif
+    if (GS_PROBE(GS_PROBE_NO_REC)) {
+      ra = rb = rc = make_float4((float)g, 0.f, 0.f, 0.f);
+    } else {
+      ra = rec[3 * g];
+      rb = rec[3 * g + 1];
+      rc = rec[3 * g + 2];
+    }
     key = (k_cur & 0xFFFFFFFF00000000ull) | ((unsigned long long)g << 8) | tid;  // g < 2^24 (slot_keys)
   }
-#ifdef GS_STAMP
-  if (tid == 0 && small) {
-    __builtin_amdgcn_s_waitcnt(0);  // (wave 0's records have arrived)
-    STAMP(1, 6);
-  }
-#endif
-  if (small) {
-#if GS_SMALL_RANK
-   if (n <= GS_SMALL_RANK) {
-    // rank counting (keys are unique): every work-item of a wave holding keys counts the keys below
-    // its own over all n in LDS (uniform reads, two keys per read, no barrier in the loop) and
-    // records its staging slot at that rank
-#if GS_RANK_MERGE
-   if (n > GS_MERGE_MIN) {
+  if (small) STAMP_WAITED(1, 6);  // (wave 0's records have arrived)
+  if (small && n > GS_MERGE_MIN) {
     // merge ranking: the wave's sorted run in LDS, ranks by binary searches of the other runs; the
     // work-item holding a sorted key (its slot in the low 8 bits) records slot and published key
     const uint32_t m = (n + 63u) >> 6;  // runs holding keys (uniform)
@@ -1991,7 +1875,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         if (q != wave) r += gs_run_below(s_key + 64u * q, sk);
     }
     __syncthreads();  // every read of the keys is done before records overwrite them
-    if (tid < n) s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
+    if (tid < n) s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, true);
     if (sk != ~0ull) {
       if (pub) {
         keys_out[range.x + r] = tbits | (sk >> 32);
@@ -1999,19 +1883,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       }
       s_sslot[r] = (uint8_t)(sk & 0xFFu);
     }
-   } else
-#endif
-   {
+  } else if (small) {
+    // rank counting (keys are unique): every work-item of a wave holding keys counts the keys below
+    // its own over all n in LDS (uniform reads, eight keys per step, no barrier in the loop) and
+    // records its staging slot at that rank
     s_key[tid] = key;  // ~0 above n
     __syncthreads();
-    uint32_t r = 0;
-#ifdef GS_PROBE_NO_RANK  // (timing probe: identity ranks, wrong image)
-    r = tid;
-    if (false) {
-#else
-    if (wave * 64u < n) {
-#endif
-      // eight keys per step, four uniform reads in flight (entries n .. 255 hold ~0: never below a key)
+    uint32_t r = GS_PROBE(GS_PROBE_NO_RANK) ? tid : 0u;
+    if (wave * 64u < n && !GS_PROBE(GS_PROBE_NO_RANK)) {
+      // four uniform reads in flight (entries n .. 255 hold ~0: never below a key)
       const uint32_t nu = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
       for (uint32_t j = 0; j < nu; j += 8) {
         const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_key + j);
@@ -2024,61 +1904,22 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     }
     __syncthreads();  // every read of the keys is done before records overwrite them
     if (tid < n) {
-      s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
+      s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, true);
       if (pub) {
         keys_out[range.x + r] = tbits | (key >> 32);
         vals_out[range.x + r] = (uint32_t)(key >> 8) & 0xFFFFFFu;
       }
       s_sslot[r] = (uint8_t)tid;
     }
-   }
-   } else
-#endif
-   {
-    // bitonic network, one key per work-item: shuffles for strides < 64, LDS for 64 / 128
-    uint32_t npad = 1;
-    while (npad < n) npad <<= 1;
-#ifdef GS_PROBE_NO_SORT
-    npad = 1;
-#endif
-    // waves wholly above npad hold only padding and skip the exchanges (they still join the
-    // barriers of the 64 / 128 strides)
-    const bool active = wave * 64u < npad;
-    for (uint32_t k = 2; k <= npad; k <<= 1)
-      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        unsigned long long other;
-        if (j >= 64) {
-          __syncthreads();
-          s_key[tid] = key;
-          __syncthreads();
-          other = s_key[tid ^ j];
-        } else {
-          if (!active) continue;
-          other = __shfl_xor(key, (int)j);
-        }
-        const bool swap = (other < key) == (((tid & j) == 0) == ((tid & k) == 0));
-        key = swap ? other : key;
-      }
-    if (npad >= 128) __syncthreads();  // the last exchange reads are done before records overwrite them
-    if (tid < n) {
-      s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc);
-      if (pub) {  // published frame only (PTGS_FLAG_SPLAT_PUBLISH): the blend needs neither
-        keys_out[range.x + tid] = tbits | (key >> 32);
-        vals_out[range.x + tid] = (uint32_t)(key >> 8) & 0xFFFFFFu;
-      }
-      s_sslot[tid] = (uint8_t)(key & 0xFFu);
-    }
-   }
   } else {
     if (mid) {
       unsigned long long* seg = fu.scap ? const_cast<unsigned long long*>(tile_slots) + range.x
                               : n <= GS_TILE_SLOTS ? const_cast<unsigned long long*>(tile_slots) + (size_t)tile * GS_TILE_SLOTS
                                                    : pairs + range.x;
       if (mid_lds) {
-        // rank by counting (keys are unique: the gaussian is in the low word): each work-item ranks
-        // its two keys against all n in LDS (uniform reads), then writes them to their ranks
-#if GS_RANK_MERGE
-        // merge ranking (above): wave w sorts runs w and w + 4 (slots tid and tid + 256)
+        // merge ranking (above), two keys per work-item: wave w sorts runs w and w + 4 (slots tid and
+        // tid + 256), then writes both keys to their ranks (keys are unique: the gaussian is in the
+        // low word)
         unsigned long long k0 = tid < n ? seg[tid] : ~0ull;
         unsigned long long k1 = tid + GS_BLOCK < n ? seg[tid + GS_BLOCK] : ~0ull;
         const uint32_t m = (n + 63u) >> 6;  // runs holding keys: 5 .. 8 (uniform)
@@ -2093,21 +1934,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
           if (q != wave) r0 += gs_run_below(run, k0);
           if (q != wave + 4u && wave + 4u < m) r1 += gs_run_below(run, k1);
         }
-#else
-        const unsigned long long k0 = tid < n ? seg[tid] : ~0ull;
-        const unsigned long long k1 = tid + GS_BLOCK < n ? seg[tid + GS_BLOCK] : ~0ull;
-        s_key[tid] = k0;
-        s_key[tid + GS_BLOCK] = k1;
-        __syncthreads();
-        uint32_t r0 = 0, r1 = 0;
-        const uint32_t nu = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
-        for (uint32_t j = 0; j < nu; j += 4) {  // (entries n .. 511 hold ~0)
-          const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(s_key + j);
-          const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(s_key + j + 2);
-          r0 += ((x.x < k0) + (x.y < k0)) + ((y.x < k0) + (y.y < k0));
-          r1 += ((x.x < k1) + (x.y < k1)) + ((y.x < k1) + (y.y < k1));
-        }
-#endif
         __syncthreads();
         if (k0 != ~0ull) s_key[r0] = k0;  // (the slots below n hold exactly the keys other than ~0)
         if (k1 != ~0ull) s_key[r1] = k1;
@@ -2146,7 +1972,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     s_stage[GS_BLOCK].c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
 
-#ifndef GS_PROBE_NO_BLEND
   const uint32_t px = tile_x * GS_BLOCK_X + (wave & 1u) * 8u + (lane & 7u);
   const uint32_t py = tile_y * GS_BLOCK_Y + (wave >> 1) * 8u + (lane >> 3);
   const bool inside = px < cam.W && py < cam.H;
@@ -2161,15 +1986,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   STAMP(1, 1);
   for (uint32_t base = 0; todo > 0; base += GS_BLOCK, todo -= GS_BLOCK) {
     // (small tiles: the barrier also publishes the records, masks and sorted slots staged after the
-    // sort; large tiles: every wave is done with the previous batch)
-#if GS_FIRST_PLAIN
-    // (the first batch: done = !inside, and every tile holds a pixel inside the image: a plain barrier
-    // instead of the counting one, which reduces through LDS behind a second barrier)
+    // sort; large tiles: every wave is done with the previous batch.) The first batch: done = !inside,
+    // and every tile holds a pixel inside the image: a plain barrier instead of the counting one, which
+    // reduces through LDS behind a second barrier.
     if (base == 0) __syncthreads();
     else if (__syncthreads_count(done) == GS_BLOCK) break;
-#else
-    if (__syncthreads_count(done) == GS_BLOCK) break;
-#endif
     const uint32_t idx = base + tid;
     if (!small) {
       if (idx < n) {
@@ -2202,9 +2023,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
             slot * (uint32_t)sizeof(GStage);
       cnt += (uint32_t)__popcll(bal);
     }
-#ifdef GS_PROBE_NO_EVAL
-    cnt = 0;
-#endif
+    if (GS_PROBE(GS_PROBE_NO_EVAL)) cnt = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2212,54 +2031,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const uint32_t cntu = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
     if (lane < 4) s_list[wave][cntu + lane] = GS_BLOCK * (uint32_t)sizeof(GStage);
     const uint32_t* list = s_list[wave];
-#if GS_EVAL_AB
-    // groups of GS_EVAL_AB entries: their records, quadratics and alphas first (independent: the
-    // reads and the exp2 chains overlap), then the transmittance chain through them in order (the only
-    // loop-carried dependency); the same operations as the one-entry form, so the image is identical
-    for (uint32_t j = 0; j < cntu; j += 4) {
-      if (__ballot(!done) == 0) break;
-      const uint4 o4 = *reinterpret_cast<const uint4*>(list + j);  // 4 list entries
-#pragma unroll
-      for (int h = 0; h < 4; h += GS_EVAL_AB) {
-        float al[GS_EVAL_AB], k0[GS_EVAL_AB], k1[GS_EVAL_AB], k2[GS_EVAL_AB];
-        bool behind[GS_EVAL_AB];
-#pragma unroll
-        for (int u = 0; u < GS_EVAL_AB; ++u) {
-          const int q = h + u;
-          const uint32_t o = q == 0 ? o4.x : q == 1 ? o4.y : q == 2 ? o4.z : o4.w;
-          const float4 a = *reinterpret_cast<const float4*>(stage + o);
-          const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
-          k2[u] = *reinterpret_cast<const float*>(stage + o + 32);
-          behind[u] = OVER && !(*reinterpret_cast<const float*>(stage + o + 44) < lim);
-          const float z = __builtin_fmaf(a.x, uxx, __builtin_fmaf(a.y, uxy, __builtin_fmaf(a.z, uyy,
-                                         __builtin_fmaf(a.w, ux, __builtin_fmaf(b.x, uy, b.y)))));
-          al[u] = z >= -7.9943534f ? fminf(0.99f, __builtin_amdgcn_exp2f(z)) : 0.0f;
-          k0[u] = b.z;
-          k1[u] = b.w;
-        }
-#pragma unroll
-        for (int u = 0; u < GS_EVAL_AB; ++u) {
-          if (OVER) done = done || behind[u];
-          const float alpha = done ? 0.0f : al[u];
-          float wgt = alpha * T;
-          float test_T = T - wgt;
-          const bool term = test_T < 0.0001f;
-#if GS_TERM_BRANCH
-          if (__ballot(term))
-#endif
-          {
-            done = done || term;
-            wgt = term ? 0.0f : wgt;
-            test_T = term ? T : test_T;
-          }
-          C0 = __builtin_fmaf(k0[u], wgt, C0);
-          C1 = __builtin_fmaf(k1[u], wgt, C1);
-          C2 = __builtin_fmaf(k2[u], wgt, C2);
-          T = test_T;
-        }
-      }
-    }
-#else
     for (uint32_t j = 0; j < cntu; j += 4) {
       // (the all-done test costs two VALU (the done mask from SGPRs to a compare): every
       // GS_DONE_EVERY entries only)
@@ -2267,44 +2038,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       const uint4 o4 = *reinterpret_cast<const uint4*>(list + j);  // 4 list entries
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-#ifdef GS_EVAL_SPLIT
-        if (u == 2) __builtin_amdgcn_sched_barrier(0);
-#endif
         const uint32_t o = u == 0 ? o4.x : u == 1 ? o4.y : u == 2 ? o4.z : o4.w;
-#if GS_EVAL_RFL
-        // one lane reads the record (the LDS returns 36 B instead of 64 x 36 B) and the values reach the
-        // wave as scalar operands through readfirstlane
-        float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = a1;
-        float c1 = 0.0f;
-        if (lane == 0) {
-          a1 = *reinterpret_cast<const float4*>(stage + o);
-          b1 = *reinterpret_cast<const float4*>(stage + o + 16);
-          c1 = *reinterpret_cast<const float*>(stage + o + 32);
-        }
-        auto rfl = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
-        const float4 a = make_float4(rfl(a1.x), rfl(a1.y), rfl(a1.z), rfl(a1.w));
-        const float4 b = make_float4(rfl(b1.x), rfl(b1.y), rfl(b1.z), rfl(b1.w));
-        const float cb = rfl(c1);
-#else
         const float4 a = *reinterpret_cast<const float4*>(stage + o);
-#endif
-#if GS_EVAL_RFL
-#elif defined(GS_PROBE_LDS_A)  // (timing probe: one LDS read per entry instead of three; wrong image, and its
-                       // coefficients end pixels early: not a clean measure of the LDS reads)
-        const float4 b = make_float4(a.w, a.z, a.y, a.x);
-        const float cb = a.y;
-#else
         const float4 b = *reinterpret_cast<const float4*>(stage + o + 16);
         const float cb = *reinterpret_cast<const float*>(stage + o + 32);
-#endif
-#if defined(GS_PROBE_LDS_X2) && !GS_EVAL_RFL  // (timing probe: 16 of a record's 36 B read twice from LDS, the copy only waited for: same image)
-        {
-          uint32_t z0 = 0;
-          asm volatile("" : "+v"(z0));
-          const float4 a2 = *reinterpret_cast<const float4*>(stage + (o ^ z0) + 16);
-          asm volatile("" ::"v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w));
-        }
-#endif
         if (OVER) {  // sorted by depth: the first Gaussian at or behind the mesh ends the pixel
           const float gd = *reinterpret_cast<const float*>(stage + o + 44);
           done = done || !(gd < lim);
@@ -2320,10 +2057,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         float wgt = alpha * T;
         float test_T = T - wgt;
         const bool term = test_T < 0.0001f;  // only a valid pair can get there
-#if GS_TERM_BRANCH
-        if (__ballot(term))  // rare: this Gaussian would saturate the pixel -> stop before it
-#endif
-        {
+        if (__ballot(term)) {  // rare: this Gaussian would saturate the pixel -> stop before it
           done = done || term;
           wgt = term ? 0.0f : wgt;
           test_T = term ? T : test_T;
@@ -2334,7 +2068,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         T = test_T;
       }
     }
-#endif
   }
   STAMP(1, 2);
   if (fu.scap && tid == 0 && n_front) fu.cursor[tile] = 0;  // (n > 0: every wave passed a barrier after reading it)
@@ -2348,14 +2081,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const size_t pix = (size_t)py2 * cam.W + px2;
     if (OVER) {
       const float4 u4 = under[pix];
-      gs_st4<GS_NT_OUT>(out + pix, make_float4(C0 + T * u4.x, C1 + T * u4.y, C2 + T * u4.z, (1.0f - T) + T * u4.w));
+      gs_st4_nt(out + pix, make_float4(C0 + T * u4.x, C1 + T * u4.y, C2 + T * u4.z, (1.0f - T) + T * u4.w));
     } else {
-      gs_st4<GS_NT_OUT>(out + pix, make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T));
+      gs_st4_nt(out + pix, make_float4(C0 + T * bg_r, C1 + T * bg_g, C2 + T * bg_b, 1.0f - T));
     }
   }
   STAMP_SYNC();
   STAMP(1, 3);
-#endif
 }
 
 // Published frame of the fused front end (PTGS_FLAG_SPLAT_PUBLISH, tests): the blend wrote each tile's
@@ -2429,7 +2161,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   cam.row_end = std::min(tile_row_end, cam.grid_y);
   if (cam.row_end < cam.row_begin) cam.row_end = cam.row_begin;
   cam.cull = (g->chunk_bounds && (cam.row_begin > 0 || cam.row_end < cam.grid_y)) ? 1u : 0u;
-  cam.tight = (GS_TIGHT_BIN && !stats && !publish) ? 1u : 0u;
+  cam.tight = (!stats && !publish) ? 1u : 0u;
   const uint32_t tiles = cam.grid_x * cam.grid_y;
 
   if ((e = ensure(w->means2d, (size_t)n * 8))) return e;
@@ -2496,6 +2228,13 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     const uint32_t demand = w->k_host[8];
     uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1u << 20, n), w->sp_cap);
     if (demand > w->sp_cap) want = std::max<uint64_t>(want, (uint64_t)demand + demand / 4u);
+    // a reported frame's own demand reaches k_host[8] only with the NEXT front end: its spilled
+    // tiles hold at most its pair count, which its blend (running or done: it raised the report) has
+    // published to k_host[0], so the pool grows to that now and this frame cannot exhaust it the same way
+    if (*report & 1u) {
+      const uint32_t k = w->k_host[0];
+      want = std::max<uint64_t>(want, (uint64_t)k + k / 4u);
+    }
     want = std::min<uint64_t>(want, 0xFFFFFFF0u);
     if (want > w->sp_cap || !w->sp_keys.p) {
       if ((e = ensure(w->sp_keys, want * 8)) || (e = ensure(w->sp_vals, want * 4))) return e;
@@ -2579,12 +2318,6 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
 #ifndef GS_FUSED_MAX_SCAP
 #define GS_FUSED_MAX_SCAP 2048u  // larger tiles (1M Gaussians at 1080p): three launches measured faster
 #endif
-#ifndef GS_FRONTEND_DEFAULT
-#define GS_FRONTEND_DEFAULT 1  // 0: always three launches
-#endif
-#ifndef GS_TILE_ORDER
-#define GS_TILE_ORDER 1  // fused frames blend their tiles heaviest first (gs_tile_order)
-#endif
 #ifndef GS_FUSED_RUNS_PER_TILE
 #define GS_FUSED_RUNS_PER_TILE 32u  // (C2 Morton order: 6; random order: 51; orbit views up to ~20, where
                                     // fused measured 0.13 vs 0.24 ms for three launches)
@@ -2597,7 +2330,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     const char* v = getenv("PTGS_GS_FRONTEND");  // "fused" / "three" (A/B switch)
     if (v && !strcmp(v, "three")) return 0;
     if (v && !strcmp(v, "fused")) return 1;
-    return GS_FRONTEND_DEFAULT ? 2 : 0;
+    return 2;
   }();
   // both front ends publish the frame's touched (workgroup, tile) runs (k_host[4]: the fused kernel's
   // reservations, the count kernel's nonzero histogram entries); the latest one decides, so the
@@ -2652,12 +2385,10 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   // the blend's tile order (heaviest tiles of the previous frame first), built by the front end's
   // first launch
   uint32_t* order = nullptr;
-#if GS_TILE_ORDER
   if (rows) {
     if ((e = ensure(w->order, (size_t)tiles * 4))) return e;
     order = (uint32_t*)w->order.p;
   }
-#endif
   const GsFused no_fu = {0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order, nullptr, 0u};
 
   auto enqueue_fused = [&]() -> hipError_t {
@@ -3076,11 +2807,4 @@ hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long**
 
 }  // namespace ptgs
 
-#ifdef GS_STAMP
-extern "C" int ptgs_debug_stamps(int kind, unsigned long long* host, unsigned int n) {
-  const size_t per = sizeof(ptgs::g_gs_stamps[0]);
-  if (n * 8ull > per) n = (unsigned int)(per / 8);
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ptgs::g_gs_stamps), (size_t)n * 8, (size_t)kind * per,
-                                  hipMemcpyDeviceToHost);
-}
-#endif
+GS_STAMP_EXPORT

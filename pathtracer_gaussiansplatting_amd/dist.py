@@ -184,16 +184,46 @@ def render_path_traced_frame(renderer, ubo, width: int, height: int, accum, spp_
     return reduce_sum(accum)
 
 
+class _DeferredReport:
+    """PTGS_EINCOMPLETE / PTGS_EINVAL from a splat call report an EARLIER frame (ptgs.h): this call's frame
+    was rendered. Raising it before the frame's collective would leave the other ranks blocked in it (a
+    multi-rank hang), so the splat calls of a sharded frame run inside this context, which holds
+    such a report until the collective has been issued (`raise_pending`). Any other error raises at once."""
+
+    def __init__(self):
+        self.err = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        from ._abi import PTGS_EINCOMPLETE, PTGS_EINVAL, PtgsError
+        if et is not None and issubclass(et, PtgsError) and ev.code in (PTGS_EINCOMPLETE, PTGS_EINVAL) \
+                and "earlier splat frame" in str(ev):
+            self.err = ev
+            return True
+        return False
+
+    def raise_pending(self):
+        if self.err is not None:
+            raise self.err
+
+
 def render_gaussian_frame(renderer, gaussians: dict, ubo, width: int, height: int, out, rank: int, world: int,
                           bg=(0.0, 0.0, 0.0), stream=None, tile_rows=None):
     """Tile-row-sharded 3DGS frame; the root gets the composed image. tile_rows: every rank's
-    (begin, end) tile rows (default: equal row counts, tile_row_shard)."""
+    (begin, end) tile rows (default: equal row counts, tile_row_shard). A report about an earlier frame of
+    this rank's workspace is raised after the row gather (every rank joins the collective)."""
     if tile_rows is None:
         tile_rows = [tile_row_shard(g, world, height) for g in range(world)]
     rows = tile_rows[rank]
+    rep = _DeferredReport()
     if rows[1] > rows[0]:
-        renderer.splat_gaussians(gaussians, ubo, width, height, out, bg=bg, tile_rows=rows, stream=stream)
-    return gather_rows(out, [pixel_rows(r, height) for r in tile_rows], dst=0, renderer=renderer, stream=stream)
+        with rep:
+            renderer.splat_gaussians(gaussians, ubo, width, height, out, bg=bg, tile_rows=rows, stream=stream)
+    img = gather_rows(out, [pixel_rows(r, height) for r in tile_rows], dst=0, renderer=renderer, stream=stream)
+    rep.raise_pending()
+    return img
 
 
 def render_hybrid_frame(renderer, gaussians: dict, ubo, width: int, height: int, accum, depth, out, spp_total: int,
@@ -225,9 +255,13 @@ def render_hybrid_frame(renderer, gaussians: dict, ubo, width: int, height: int,
     p0, p1 = px[rank]
     if p1 > p0:  # the primary-hit depth of this rank's rows only (the composite reads no other)
         renderer.trace_depth(ubo, width, height, depth, stream=stream, rows=(p0, p1))
+    rep = _DeferredReport()
     if p1 > p0:
         with _on_stream(out, stream):
             out[p0:p1] = resolve_mean(accum[p0:p1])
-        renderer.splat_gaussians(gaussians, ubo, width, height, out, tile_rows=tile_rows[rank], over=(depth, out),
-                                 stream=stream, **splat_kw)
-    return gather_rows(out, px, dst=0, renderer=renderer, stream=stream)
+        with rep:
+            renderer.splat_gaussians(gaussians, ubo, width, height, out, tile_rows=tile_rows[rank],
+                                     over=(depth, out), stream=stream, **splat_kw)
+    img = gather_rows(out, px, dst=0, renderer=renderer, stream=stream)
+    rep.raise_pending()  # (after the collective: see _DeferredReport)
+    return img

@@ -100,3 +100,32 @@ def test_rccl_unique_id_without_gpu(native_lib):
     assert native_lib.ptgs_comm_unique_id(buf) == 0
     assert any(bytes(buf))
     assert native_lib.ptgs_comm_unique_id(None) == -1  # PTGS_EINVAL
+
+
+def _compile_layout(include_dir, cxx=False):
+    import subprocess
+    src = os.path.join(ROOT, "tests", "native", "abi_layout.c")
+    cmd = (["g++", "-std=c++17", "-x", "c++"] if cxx else ["gcc", "-std=c11", "-pedantic-errors"])
+    cmd += ["-Wall", "-Werror", "-fsyntax-only", "-I", include_dir, src]
+    return subprocess.run(cmd, capture_output=True, text=True)
+
+
+def test_header_layouts_compile_in_c_and_cxx():
+    """include/ptgs/ptgs.h's static layout asserts (GeneralHeaders.h sizes / offsets) hold as C11 and C++."""
+    inc = os.path.join(ROOT, "include")
+    for cxx in (False, True):
+        r = _compile_layout(inc, cxx)
+        assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.parametrize("old,new", [("float pad1;", "float pad1, extra;"),
+                                     ("int32_t sg_id;", "int64_t sg_id;"),
+                                     ("uint32_t frame_count;", "uint64_t frame_count;")])
+def test_header_layout_drift_fails_to_compile(tmp_path, old, new):
+    """A drifted copy of the header (one field changed) must not compile: the asserts are live."""
+    text = open(HEADERS[0]).read()
+    assert old in text
+    (tmp_path / "ptgs").mkdir()
+    (tmp_path / "ptgs" / "ptgs.h").write_text(text.replace(old, new, 1))
+    r = _compile_layout(str(tmp_path))
+    assert r.returncode != 0 and "static assert" in r.stderr.lower(), r.stderr

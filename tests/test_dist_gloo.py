@@ -260,3 +260,71 @@ def test_dist_render_hybrid_frame_gloo(world, oracle_lib, native_lib):
     assert hits > 50, hits  # the Gaussians change the frame
     assert err < 1e-5, err
 
+
+
+class _ReportingRenderer(_OracleRenderer):
+    """A rank whose splat call renders its rows and then reports an EARLIER incomplete frame, as
+    ptgs_splat_gaussians does with PTGS_EINCOMPLETE (ptgs.h): the frame is rendered, the code is news."""
+
+    def splat_gaussians(self, *a, **kw):
+        from pathtracer_gaussiansplatting_amd._abi import PTGS_EINCOMPLETE, PtgsError
+        super().splat_gaussians(*a, **kw)
+        raise PtgsError("ptgs_splat_gaussians failed: PTGS_EINCOMPLETE an earlier splat frame left tiles "
+                        "incomplete (spill pool exhausted; grown)", PTGS_EINCOMPLETE)
+
+
+def _report_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        import scenes_util as U
+        from pathtracer_gaussiansplatting_amd import Camera, make_ubo
+        from pathtracer_gaussiansplatting_amd import dist as D
+        from pathtracer_gaussiansplatting_amd import synthetic as Y
+        from pathtracer_gaussiansplatting_amd._abi import PTGS_EINCOMPLETE, PtgsError
+        sc = U.cornell()
+        r = _ReportingRenderer(sc) if rank == 1 else _OracleRenderer(sc)
+        GW, GH = 64, 48
+        g = {k: torch.from_numpy(v) for k, v in Y.gaussians_c2(800, seed=9).items()}
+        gu = make_ubo(Camera(aspect=GW / GH).look_at([0, 0, 0], [0, 0, -1]), sc, 0)
+        out = torch.full((GH, GW, 4), -1.0, dtype=torch.float32)
+        code = 0
+        try:
+            D.render_gaussian_frame(r, g, gu, GW, GH, out, rank, world)
+        except PtgsError as e:
+            code = e.code
+        if rank == 0:
+            full = oracle.splat_gaussians({k: v.numpy() for k, v in g.items()}, gu, GW, GH)
+            q.put(("ok", code, bool(np.array_equal(out.numpy(), full["image"]))))
+        else:
+            q.put(("rank1", code == PTGS_EINCOMPLETE))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", traceback.format_exc()))
+
+
+def test_dist_splat_report_does_not_hang_gloo():
+    """a rank whose splat call reports an earlier incomplete frame (PTGS_EINCOMPLETE) still
+    joins the row gather (the report is raised after it), so rank 0 gets the whole frame and nothing hangs."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_report_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict()
+    for _ in range(world):
+        m = q.get(timeout=180)
+        assert m[0] != "err", m[1]
+        res[m[0]] = m[1:]
+    for p in procs:
+        p.join(timeout=60)
+    assert res["ok"] == (0, True), res
+    assert res["rank1"] == (True,), res

@@ -254,6 +254,46 @@ def test_gaussians_spill_pool_exhausted_is_reported(native_lib):
         rc.close()
 
 
+def test_gaussians_views_pool_exhausted_renders_every_view(native_lib):
+    """a views call whose view v >= 1 reports an earlier incomplete frame still renders every
+    view (the report is returned after all of them are enqueued), and the reporting call's own frames are
+    complete. Two views of the exhausting frame above on a fresh context: both are incomplete; the next
+    views call returns PTGS_EINCOMPLETE with both outputs equal to the exact frame."""
+    from pathtracer_gaussiansplatting_amd import Renderer, PtgsError
+    from pathtracer_gaussiansplatting_amd._abi import PTGS_EINCOMPLETE
+    W, H = 1920, 1080
+    g = Y.gaussians_c2(2000, seed=45)
+    g["scales"] *= np.float32(60.0)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    dg = {k: _dev(v) for k, v in g.items()}
+    rb = Renderer(0)
+    try:
+        exact = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        rb.splat_gaussians(dg, ubo, W, H, exact, want_stats=True)
+    finally:
+        rb.close()
+    ra = Renderer(0)
+    try:
+        outs = [torch.zeros_like(exact) for _ in range(2)]
+        ra.splat_gaussians_views(dg, [ubo, ubo], W, H, outs)  # both views exhaust their pools
+        torch.cuda.synchronize()
+        outs = [torch.full_like(exact, -3.0) for _ in range(2)]
+        with pytest.raises(PtgsError) as ei:
+            ra.splat_gaussians_views(dg, [ubo, ubo], W, H, outs)
+        assert ei.value.code == PTGS_EINCOMPLETE
+        torch.cuda.synchronize()
+        for v, o in enumerate(outs):  # (before the fix view 0 was never enqueued: still -3)
+            assert torch.equal(o, exact), f"view {v} not rendered completely"
+        st = ra.splat_status()
+        assert st.views[0] + st.views[1] >= 1 and st.incomplete_tiles > 0
+        ra.splat_gaussians_views(dg, [ubo, ubo], W, H, outs)  # nothing more to report
+        st = ra.splat_status()
+        assert st.frames == 0 and st.incomplete_tiles == 0
+        assert all(torch.equal(o, exact) for o in outs)
+    finally:
+        ra.close()
+
+
 def test_gaussians_out_of_range_ids_are_reported(native_lib, oracle_lib):
     """ids must be a permutation of [0, N). An id >= N is never used as an index (the
     Gaussian is dropped: no out-of-bounds write) and the next call returns PTGS_EINVAL."""
