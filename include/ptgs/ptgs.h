@@ -412,6 +412,11 @@ typedef struct ptgs_trace_stats {
 #define PTGS_FLAG_SPLAT_PUBLISH 8u   /* ptgs_splat_gaussians also writes the sorted keys / values of every
                                       * tile (ptgs_splat_get_buffers; parity tests): off in production,
                                       * the blend needs neither */
+#define PTGS_FLAG_SPLAT_PUBLISH_TIGHT 64u /* with PTGS_FLAG_SPLAT_PUBLISH (tests): published frames bin each
+                                      * Gaussian like the stream-ordered frames do — only to the tiles its
+                                      * alpha >= 1/255 box overlaps, not its whole 3-sigma rectangle — so the
+                                      * timed path's keys / values / ranges can be compared with the oracle's
+                                      * tight mode (oracle_splat_gaussians_tight). Same image either way. */
 #define PTGS_FLAG_PT_WAVEFRONT 16u  /* ptgs_trace_camera runs the wavefront path tracer (raygen / extend /
                                       * shade / shadow / accumulate stages over compacted ray queues)
                                       * instead of the one-kernel-per-frame path loop; same image, same

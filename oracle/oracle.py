@@ -58,6 +58,8 @@ def lib() -> C.CDLL:
         L.oracle_splat_gaussians.argtypes = [_P, _P, _P, _P, _P, _U, _P, _U, _U, _P, _P, _P, _U, _U, _P, _P, _P, _P, _P,
                                              C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)), _P,
                                              _P]
+        L.oracle_splat_gaussians_tight.restype = C.c_int
+        L.oracle_splat_gaussians_tight.argtypes = L.oracle_splat_gaussians.argtypes
         L.oracle_free.restype = None
         L.oracle_free.argtypes = [_P]
         L.oracle_knn3_mean_dist2.restype = None
@@ -127,8 +129,10 @@ def trace_depth(desc, ubo, width, height, threads=0) -> np.ndarray:
     return out
 
 
-def splat_gaussians(g: dict, ubo, width, height, bg=(0.0, 0.0, 0.0), tile_rows=None, over=None):
-    """over=(depth (H, W) float32, under (H, W, 4) float32): the hybrid composite."""
+def splat_gaussians(g: dict, ubo, width, height, bg=(0.0, 0.0, 0.0), tile_rows=None, over=None, tight=False):
+    """over=(depth (H, W) float32, under (H, W, 4) float32): the hybrid composite. tight: bin by the
+    alpha >= 1/255 box as the product's stream-ordered (timed) frames do (oracle_splat_gaussians_tight);
+    default: the 3-sigma rectangles of published / stats frames."""
     n = g["means"].shape[0]
     arrs = {k: np.ascontiguousarray(v, np.float32) for k, v in g.items()}
     radii = np.zeros(n, np.int32)
@@ -147,7 +151,8 @@ def splat_gaussians(g: dict, ubo, width, height, bg=(0.0, 0.0, 0.0), tile_rows=N
     if over is not None:
         dl = np.ascontiguousarray(over[0], np.float32)
         un = np.ascontiguousarray(over[1], np.float32)
-    K = lib().oracle_splat_gaussians(arrs["means"].ctypes.data, arrs["scales"].ctypes.data,
+    fn = lib().oracle_splat_gaussians_tight if tight else lib().oracle_splat_gaussians
+    K = fn(arrs["means"].ctypes.data, arrs["scales"].ctypes.data,
                                      arrs["rotations"].ctypes.data, arrs["opacities"].ctypes.data,
                                      arrs["colors"].ctypes.data, n, C.addressof(ubo), width, height, bgc.ctypes.data,
                                      None if dl is None else dl.ctypes.data, None if un is None else un.ctypes.data,

@@ -27,6 +27,7 @@ FLAG_GPU_BVH = 4
 FLAG_GPU_LBVH = 32
 FLAG_SPLAT_PUBLISH = 8
 FLAG_PT_WAVEFRONT = 16
+FLAG_SPLAT_PUBLISH_TIGHT = 64  # tests: published frames bin like the stream-ordered (timed) frames
 
 # ---------------------------------------------------------------------------------------------
 # numpy dtypes for the array structs (byte-compatible with Helpers/GeneralHeaders.h)

@@ -645,7 +645,8 @@ static int splat_render(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
   mat4_mul(ubo->proj, ubo->view, mvp);
   hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, depth, under,
                                  tile_row_begin, tile_row_end, out, stats, (c->flags & PTGS_FLAG_TIME_STAGES) != 0,
-                                 (c->flags & PTGS_FLAG_SPLAT_PUBLISH) != 0, (hipStream_t)stream, report);
+                                 (c->flags & PTGS_FLAG_SPLAT_PUBLISH) != 0, (c->flags & PTGS_FLAG_SPLAT_PUBLISH_TIGHT) != 0,
+                                 (hipStream_t)stream, report);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_gaussians: %s", hipGetErrorString(e));
   return PTGS_OK;
 }

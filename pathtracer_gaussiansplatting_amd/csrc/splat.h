@@ -17,7 +17,7 @@ void splat_workspace_destroy(SplatWorkspace* w);
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
-                           ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s,
+                           ptgs_splat_stats* stats, bool time_stages, bool publish, bool publish_tight, hipStream_t s,
                            uint32_t* report);  // report: bit 0 an earlier frame was left incomplete, bit 1 ids >= N
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
 // 3D Morton order of the means: a reordered copy + the original indices (synchronises s)

@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 
@@ -46,6 +47,9 @@ struct SplatCam {
   uint32_t row_begin, row_end;  // tile rows
   uint32_t cull;                // tile rows restricted and chunk bounds given: PreArgs.cskip is valid
   uint32_t tight;               // bin by the alpha box (frames without stats / published buffers)
+  uint32_t rowcull;             // tile rows restricted: Gaussians whose radius bound misses them skip the rest
+  float fmax2;                  // max(fx^2, fy^2)
+  float w2;                     // an upper bound of the view rotation's squared spectral norm (1 for lookAt)
 };
 
 struct DevBuf {
@@ -145,6 +149,37 @@ __device__ __forceinline__ void gs_st4_nt(float4* p, const float4& v) {
   typedef float f4v __attribute__((ext_vector_type(4)));
   __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
 }
+// (Write-through (sc1) stores, which leave the XCD's L2 at once instead of at the kernel-end release,
+// measured slower for every output: image 0.0633, key rows 0.0585, records 0.0603, all 0.0679 vs 0.0565 ms.)
+
+// Upper bound (px) of the 3-sigma radius of a Gaussian of largest scale s at view-space point (x, y, d),
+// d > 0.2: radius = ceil(3 sqrt(l1)) with l1 <= lambda_max(cov) + sqrt(0.1) (the max(0.1, .) clamp of
+// gs_preprocess_one), cov = T Sigma T^T + 0.3 I, T = J W, so lambda_max(cov) <= |J|_2^2 |W|_2^2 s^2 + 0.3
+// with |J|_2^2 = max(fx, fy)^2 (1 + a^2 + b^2) / d^2 (J = diag(fx, fy) / d [[1, 0, -a], [0, 1, -b]], a and b
+// the clamped x / d and y / d of the EWA Jacobian). 1% and 2 px absorb the float rounding of both sides.
+__device__ __forceinline__ float gs_radius_bound(const SplatCam& cam, float a, float b, float d, float s) {
+  const float lam = cam.fmax2 * ((1.0f + a * a) + b * b) / (d * d) * cam.w2 * (s * s);
+  return 3.0f * sqrtf(1.01f * (lam + 0.62f)) + 2.0f;
+}
+
+// Row pre-cull of a tile-row-restricted frame (cam.rowcull): from the mean and the scales only (one load
+// round trip before the rotation / opacity / colour loads), true when the Gaussian cannot reach the
+// frame's tile rows: its rect rows [(int)((y - r) / 16), (int)((y + r + 15) / 16)) miss [row_begin,
+// row_end) for every r <= the radius bound (the exact rect is then empty: the skip is exact). False for
+// d <= 0.2 and non-finite values (the exact path decides).
+__device__ __forceinline__ bool gs_row_miss(const SplatCam& cam, float mx, float my, float mz, float sx, float sy,
+                                            float sz) {
+  const v4 pv = mv4(cam.view, mx, my, mz, 1.0f);
+  const float d = -pv.z;
+  if (!(d > 0.2f)) return false;
+  const v4 ph = mv4(cam.mvp, mx, my, mz, 1.0f);
+  const float y = ndc2pix(ph.y * (1.0f / (ph.w + 0.0000001f)), (int)cam.H);
+  const float limx = 1.3f * cam.tan_fovx, limy = 1.3f * cam.tan_fovy;
+  const float a = fminf(limx, fmaxf(-limx, pv.x / d)), b = fminf(limy, fmaxf(-limy, pv.y / d));
+  const float R = gs_radius_bound(cam, a, b, d, fmaxf(fabsf(sx), fmaxf(fabsf(sy), fabsf(sz))));
+  const float t = (float)GS_BLOCK_Y;
+  return (y + R + t < t * (float)cam.row_begin) || (y - R - t > t * (float)cam.row_end);
+}
 
 // One Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T, EWA Sigma' = J W Sigma W^T J^T + 0.3,
 // conic, 3-sigma radius, tile rect (returned; empty if culled) and, with STORE, every per-Gaussian
@@ -169,22 +204,38 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   // walk, at i) and radii / touched / means2d / conic (ptgs_splat_get_buffers) when their pointers are
   // set (the fused path without PTGS_FLAG_SPLAT_PUBLISH leaves them out)
   const uint32_t o = A.ids ? A.ids[i] : i;
-  // every input is loaded here, with the id and before the id check and the depth test: one memory round
-  // trip per Gaussian (loads behind either branch were issued only once the id / the means had arrived)
   float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
-  float qr = rots[4 * i], qx = rots[4 * i + 1], qy = rots[4 * i + 2], qz = rots[4 * i + 3];
   float sx = scales[3 * i], sy = scales[3 * i + 1], sz = scales[3 * i + 2];
-  float op = opac[i];
-  float cr = 0.0f, cg = 0.0f, cbl = 0.0f;
-  if (STORE) {
-    cr = colors[3 * i];
-    cg = colors[3 * i + 1];
-    cbl = colors[3 * i + 2];
-    asm volatile("" : "+v"(cr), "+v"(cg), "+v"(cbl));
+  float qr = 0.0f, qx = 0.0f, qy = 0.0f, qz = 0.0f, op = 0.0f, cr = 0.0f, cg = 0.0f, cbl = 0.0f;
+  bool miss = false;
+  if (!cam.rowcull) {
+    // every input is loaded here, with the id and before the id check and the depth test: one memory round
+    // trip per Gaussian (loads behind either branch were issued only once the id / the means had arrived)
+    qr = rots[4 * i]; qx = rots[4 * i + 1]; qy = rots[4 * i + 2]; qz = rots[4 * i + 3];
+    op = opac[i];
+    if (STORE) {
+      cr = colors[3 * i];
+      cg = colors[3 * i + 1];
+      cbl = colors[3 * i + 2];
+      asm volatile("" : "+v"(cr), "+v"(cg), "+v"(cbl));
+    }
+    // (the empty asm needs the values here, so the compiler cannot sink the loads behind the branches)
+    asm volatile("" : "+v"(mx), "+v"(my), "+v"(mz), "+v"(qr), "+v"(qx), "+v"(qy), "+v"(qz), "+v"(sx), "+v"(sy),
+                 "+v"(sz), "+v"(op));
+  } else {
+    // a tile-row shard: most Gaussians miss its rows; the rest of the inputs are loaded only for those
+    // whose radius bound reaches them (a second round trip for them, none for the others)
+    miss = gs_row_miss(cam, mx, my, mz, sx, sy, sz);
+    if (!miss) {
+      qr = rots[4 * i]; qx = rots[4 * i + 1]; qy = rots[4 * i + 2]; qz = rots[4 * i + 3];
+      op = opac[i];
+      if (STORE) {
+        cr = colors[3 * i];
+        cg = colors[3 * i + 1];
+        cbl = colors[3 * i + 2];
+      }
+    }
   }
-  // (the empty asm needs the values here, so the compiler cannot sink the loads behind the branches)
-  asm volatile("" : "+v"(mx), "+v"(my), "+v"(mz), "+v"(qr), "+v"(qx), "+v"(qy), "+v"(qz), "+v"(sx), "+v"(sy),
-               "+v"(sz), "+v"(op));
   if (STORE && rects) rects[i] = none;  // empty rect: the scatter reads rects only
   if (o >= A.n) {  // ids must be a permutation of [0, n): an index outside it is dropped, not written
     if (STORE) __atomic_store_n(A.bad_ids, 1u, __ATOMIC_RELAXED);  // (reported by the next call)
@@ -194,6 +245,7 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
     radii[o] = 0;
     touched[o] = 0;
   }
+  if (miss) return none;
   // frustum: view-space depth d = -z (RH, camera looks down -Z)
   v4 pv = mv4(cam.view, mx, my, mz, 1.0f);
   float d = -pv.z;
@@ -333,13 +385,19 @@ __device__ __forceinline__ bool gs_chunk_misses(const SplatCam& cam, const float
   }
   if (dmax < 0.19f) return true;                // every Gaussian is culled by the near test
   if (dmin < 0.25f || !front) return false;     // too close to bound the projection
-  const float *V = cam.view;
-  const float wf2 = ((V[0] * V[0] + V[1] * V[1]) + V[2] * V[2]) + ((V[4] * V[4] + V[5] * V[5]) + V[6] * V[6]) +
-                    ((V[8] * V[8] + V[9] * V[9]) + V[10] * V[10]);
-  const float tx = 1.3f * cam.tan_fovx, ty = 1.3f * cam.tan_fovy;
-  const float jf2 = (cam.fx * cam.fx * (1.0f + tx * tx) + cam.fy * cam.fy * (1.0f + ty * ty)) / (dmin * dmin);
-  const float lam = jf2 * wf2 * lo.w * lo.w;
-  const float R = 3.0f * sqrtf(1.01f * (lam + 0.62f)) + 3.0f;  // px
+  // the largest |x / d|, |y / d| over the box: at its corners (x / d is linear-fractional, d > 0 on the box),
+  // clamped like the EWA Jacobian's; the radius bound of gs_radius_bound at the nearest depth
+  float amax = 0.0f, bmax = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float x = (k & 1) ? hi.x : lo.x, y = (k & 2) ? hi.y : lo.y, z = (k & 4) ? hi.z : lo.z;
+    const v4 pv = mv4(cam.view, x, y, z, 1.0f);
+    amax = fmaxf(amax, fabsf(pv.x / -pv.z));
+    bmax = fmaxf(bmax, fabsf(pv.y / -pv.z));
+  }
+  amax = fminf(amax * 1.001f, 1.3f * cam.tan_fovx);
+  bmax = fminf(bmax * 1.001f, 1.3f * cam.tan_fovy);
+  const float R = gs_radius_bound(cam, amax, bmax, dmin * 0.999f, lo.w) + 1.0f;  // px
   if (!isfinite(R)) return false;
   const float t = (float)GS_BLOCK_Y;
   const float r0 = floorf((ymin - R) / t) - 1.0f, r1 = floorf((ymax + R + t) / t) + 1.0f;  // rows [r0, r1]
@@ -407,13 +465,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
+// The bands cover the frame's tile rows [row0, row1) only (a tile-row shard bins its own rows: one band of
+// up to GS_MAX_CHUNKS chunks instead of the whole frame's bands); the 64-tile groups start at row0's first
+// tile. hist, tile_info and ranges keep the frame's global tile ids (tiles = grid_x * grid_y).
 struct BinGrid {
-  uint32_t band_rows, bands, chunks, chunk, grid_x, grid_y, tiles, groups;
+  uint32_t band_rows, bands, chunks, chunk, grid_x, grid_y, tiles, groups, row0, row1;
 };
 
 __device__ __forceinline__ void gs_band(const BinGrid& bg, uint32_t& ty0, uint32_t& ty1) {
-  ty0 = blockIdx.x * bg.band_rows;
-  ty1 = min(bg.grid_y, ty0 + bg.band_rows);
+  ty0 = bg.row0 + blockIdx.x * bg.band_rows;
+  ty1 = min(bg.row1, ty0 + bg.band_rows);
 }
 
 // Pairs of one wave's 64 entries (gaussian g, x0 | w << 16, y0 | h << 16; h = 0: none), walked 64 per
@@ -674,8 +735,8 @@ __global__ __launch_bounds__(GS_COLSCAN_THREADS) void gs_bin_colscan_kernel(BinG
                                                              uint32_t* __restrict__ large_ctr) {
   __shared__ uint32_t s_ws[GS_COLSCAN_WAVES][64];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint32_t t = blockIdx.x * 64u + lane;
-  const bool ok = t < bg.tiles;
+  const uint32_t t = bg.row0 * bg.grid_x + blockIdx.x * 64u + lane;
+  const bool ok = t < bg.row1 * bg.grid_x;
   const uint32_t cpw = (bg.chunks + GS_COLSCAN_WAVES - 1u) / GS_COLSCAN_WAVES, c0 = wave * cpw,
                  c1 = min(bg.chunks, c0 + cpw);
   // all of this wave's rows in flight at once (cpw <= 64: registers, fully unrolled)
@@ -777,12 +838,18 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
     __threadfence_system();  // visible to the host before the kernel ends (the K event has no system fence)
   }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && (bg.row0 > 0 || bg.row1 < bg.grid_y)) {
+    // a tile-row frame's bands cover its rows only: the other tiles' ranges are empty (as the oracle's)
+    const uint32_t tb = bg.row0 * bg.grid_x, te = bg.row1 * bg.grid_x;
+    for (uint32_t t = tid; t < bg.tiles; t += GS_BIN_THREADS)
+      if (t < tb || t >= te) ranges[t] = make_uint2(0u, 0u);
+  }
   // (K above the pair buffer: the tiles whose segment ends beyond it keep none of their pairs here and
   // are rendered by the blend through gs_spill_tile; the fixed rows of small tiles always fit)
   for (uint32_t k = tid; k < nt; k += GS_BIN_THREADS) {
     const uint32_t t = t0 + k;
     const uint2 ti = tile_info[t];
-    const uint32_t start = s_gpre[t >> 6] + ti.x;
+    const uint32_t start = s_gpre[(t - bg.row0 * bg.grid_x) >> 6] + ti.x;
     s_cur[k] = hist[(size_t)c * bg.tiles + t];
     // where the tile's pairs go: its fixed GS_TILE_SLOTS-slot row when they fit (the blend then
     // loads keys without waiting for the range), else its segment of the pair buffer (flag bit 31)
@@ -1022,7 +1089,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
       slice = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_job[3]);
     }
     const uint32_t band = wg % gridDim.x, chunk = wg / gridDim.x;
-    const uint32_t ty0 = band * bg.band_rows, ty1 = min(bg.grid_y, ty0 + bg.band_rows);
+    const uint32_t ty0 = bg.row0 + band * bg.band_rows, ty1 = min(bg.row1, ty0 + bg.band_rows);
     const uint32_t i = chunk * bg.chunk + threadIdx.x;  // chunk <= GS_FUSED_THREADS (host)
     const bool own = threadIdx.x < bg.chunk && i < A.n;
     const bool store = owner && band == 0;
@@ -2137,7 +2204,7 @@ __global__ __launch_bounds__(256) void gs_publish_copy_kernel(const uint2* __res
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
-                           ptgs_splat_stats* stats, bool time_stages, bool publish, hipStream_t s,
+                           ptgs_splat_stats* stats, bool time_stages, bool publish, bool publish_tight, hipStream_t s,
                            uint32_t* report) {
   hipError_t e;
   *report = 0;
@@ -2160,8 +2227,20 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   cam.row_begin = std::min(tile_row_begin, cam.grid_y);
   cam.row_end = std::min(tile_row_end, cam.grid_y);
   if (cam.row_end < cam.row_begin) cam.row_end = cam.row_begin;
-  cam.cull = (g->chunk_bounds && (cam.row_begin > 0 || cam.row_end < cam.grid_y)) ? 1u : 0u;
-  cam.tight = (!stats && !publish) ? 1u : 0u;
+  cam.rowcull = (cam.row_begin > 0 || cam.row_end < cam.grid_y) ? 1u : 0u;
+  cam.cull = (g->chunk_bounds && cam.rowcull) ? 1u : 0u;
+  cam.fmax2 = std::max(cam.fx * cam.fx, cam.fy * cam.fy);
+  {  // |W|_2^2 <= the largest Gershgorin row sum of W W^T (W: the view's rotation part; 1 for a lookAt view)
+    double ww[3][3], w2 = 0.0;
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c)
+        ww[r][c] = (double)view[r] * view[c] + (double)view[4 + r] * view[4 + c] + (double)view[8 + r] * view[8 + c];
+    for (int r = 0; r < 3; ++r) w2 = std::max(w2, std::fabs(ww[r][0]) + std::fabs(ww[r][1]) + std::fabs(ww[r][2]));
+    cam.w2 = (float)(w2 * (1.0 + 1e-5));
+  }
+  // stream-ordered frames bin by the alpha box; stats / published frames by the 3-sigma rectangles, unless
+  // PTGS_FLAG_SPLAT_PUBLISH_TIGHT asks for the timed frames' binning (parity tests of their integer outputs)
+  cam.tight = ((!stats && !publish) || (publish && publish_tight)) ? 1u : 0u;
   const uint32_t tiles = cam.grid_x * cam.grid_y;
 
   if ((e = ensure(w->means2d, (size_t)n * 8))) return e;
@@ -2180,10 +2259,13 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   bgrid.grid_x = cam.grid_x;
   bgrid.grid_y = cam.grid_y;
   bgrid.tiles = tiles;
-  bgrid.groups = (tiles + 63u) / 64u;
-  if (bgrid.groups > GS_MAX_GROUPS) return hipErrorInvalidValue;
-  bgrid.band_rows = std::max(1u, std::min(cam.grid_y, GS_BAND_TILES / cam.grid_x));
-  bgrid.bands = std::max(1u, (cam.grid_y + bgrid.band_rows - 1) / bgrid.band_rows);
+  if ((tiles + 63u) / 64u > GS_MAX_GROUPS) return hipErrorInvalidValue;
+  bgrid.row0 = cam.row_begin;
+  bgrid.row1 = cam.row_end;
+  const uint32_t brows = cam.row_end - cam.row_begin;  // the frame's tile rows (the bands cover these)
+  bgrid.groups = std::max(1u, (brows * cam.grid_x + 63u) / 64u);
+  bgrid.band_rows = std::max(1u, std::min(std::max(brows, 1u), GS_BAND_TILES / cam.grid_x));
+  bgrid.bands = std::max(1u, (brows + bgrid.band_rows - 1) / bgrid.band_rows);
   bgrid.chunks = std::max(1u, std::min({(uint32_t)GS_MAX_CHUNKS, (n + GS_CHUNK_MIN - 1) / GS_CHUNK_MIN,
                                         std::max(1u, 256u / bgrid.bands)}));
   bgrid.chunk = std::max(1u, (n + bgrid.chunks - 1) / bgrid.chunks);

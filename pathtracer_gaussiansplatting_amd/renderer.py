@@ -60,11 +60,15 @@ class Renderer:
     def __init__(self, device: int = 0, lib_path: str | None = None, publish_splat_buffers: bool = False,
                  wavefront: bool = False):
         """publish_splat_buffers: every synchronised splat (want_stats) also publishes its sorted
-        keys / values for splat_buffers() (PTGS_FLAG_SPLAT_PUBLISH); wavefront: trace_camera runs the
-        wavefront path tracer (PTGS_FLAG_PT_WAVEFRONT). Both are kept across set_flags."""
+        keys / values for splat_buffers() (PTGS_FLAG_SPLAT_PUBLISH); "tight": and bins them like the
+        stream-ordered frames (PTGS_FLAG_SPLAT_PUBLISH_TIGHT, parity tests of the timed path); wavefront:
+        trace_camera runs the wavefront path tracer (PTGS_FLAG_PT_WAVEFRONT). All are kept across set_flags."""
         self.lib = _abi.load_library(lib_path)
-        self._publish = (_abi.FLAG_SPLAT_PUBLISH if publish_splat_buffers else 0) | (
-            _abi.FLAG_PT_WAVEFRONT if wavefront else 0)
+        self._publish = _abi.FLAG_PT_WAVEFRONT if wavefront else 0
+        if publish_splat_buffers:
+            self._publish |= _abi.FLAG_SPLAT_PUBLISH
+        if publish_splat_buffers == "tight":
+            self._publish |= _abi.FLAG_SPLAT_PUBLISH_TIGHT
         h = C.c_void_p()
         rc = self.lib.ptgs_create(int(device), C.byref(h))
         _abi.check(rc, f"ptgs_create(device={device})")

@@ -328,3 +328,61 @@ def test_dist_splat_report_does_not_hang_gloo():
         p.join(timeout=60)
     assert res["ok"] == (0, True), res
     assert res["rank1"] == (True,), res
+
+
+def _pipeline_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import oracle
+        import scenes_util as U
+        from pathtracer_gaussiansplatting_amd import Camera, make_ubo
+        from pathtracer_gaussiansplatting_amd import dist as D
+        from pathtracer_gaussiansplatting_amd import synthetic as Y
+        sc = U.cornell()
+        r = _OracleRenderer(sc)
+        GW, GH = 80, 60
+        g = {k: torch.from_numpy(v) for k, v in Y.gaussians_c2(1200, seed=13).items()}
+        ubos = [make_ubo(Camera(aspect=GW / GH).look_at([0.3 * f, 0.1 * f, 0.0], [0.2 * f, 0.0, -1.0]), sc, 0)
+                for f in range(4)]
+        full0 = oracle.splat_gaussians({k: v.numpy() for k, v in g.items()}, ubos[0], GW, GH)
+        tiles_x = (GW + 15) // 16
+        rows = D.balanced_tile_rows(D.row_pairs_from_ranges(full0["ranges"], tiles_x), world, tiles_x)
+        pipe = D.RowGatherPipeline(r, GW, GH, rows, rank, world, device="cpu", bg=(0.1, 0.2, 0.3))
+        got = []
+        for u in ubos:
+            img = pipe.submit(g, u)
+            pipe.wait(img)
+            got.append(img.clone())
+        if rank == 0:
+            same = []
+            for u, im in zip(ubos, got):
+                ref = oracle.splat_gaussians({k: v.numpy() for k, v in g.items()}, u, GW, GH, bg=(0.1, 0.2, 0.3))
+                same.append(bool(np.array_equal(im.numpy(), ref["image"])))
+            q.put(("ok", same, rows))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", traceback.format_exc()))
+
+
+def test_row_gather_pipeline_gloo():
+    """VERDICT r4 next #3c: the pipelined tile-row frames (dist.RowGatherPipeline: frame f's row gather
+    overlapped with frame f + 1's band, two alternating images) compose, on rank 0, the single-process
+    frames of a moving camera bit for bit (world 2, gloo, the oracle as each rank's renderer)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+    assert res[0] == "ok", res[1]
+    assert res[1] == [True] * 4, res

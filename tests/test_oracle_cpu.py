@@ -176,3 +176,40 @@ def test_oracle_over_composite_reduces_to_plain_splat(oracle_lib):
     assert np.array_equal(over["image"][..., 3], plain["image"][..., 3])
     hidden = oracle_lib.splat_gaussians(g, ubo, W, H, over=(np.zeros((H, W), np.float32), under))
     assert np.array_equal(hidden["image"], under)
+
+
+@pytest.mark.parametrize("shape", ["c2", "thin_faint", "close"])
+def test_gs_tight_binning_is_a_subset_with_invisible_drops(oracle_lib, shape):
+    """The oracle's tight mode (the alpha >= 1/255 box binning of the product's timed frames, restated in
+    oracle_splat_gaussians_tight): its (tile, gaussian) pairs are a subset of the 3-sigma rectangles'
+    pairs, every dropped pair has alpha < 1/255 at all 256 pixels of its tile (float64 check: the box's
+    margins are conservative), and the image is the same bit for bit."""
+    W, H, n = 160, 96, 3000
+    g = Y.gaussians_c2(n, seed=31)
+    eye = [0.0, 0.0, 0.0]
+    if shape == "thin_faint":
+        g["scales"][:, 0] *= np.float32(6.0)
+        g["scales"][:, 1] *= np.float32(0.05)
+        g["opacities"] = (g["opacities"] * np.float32(0.05)).astype(np.float32)
+    elif shape == "close":
+        eye = [0.0, 0.0, -2.5]
+    ubo = make_ubo(Camera(aspect=W / H).look_at(eye, [eye[0], eye[1], eye[2] - 1.0]), U.cornell(), 0)
+    full = oracle_lib.splat_gaussians(g, ubo, W, H)
+    tight = oracle_lib.splat_gaussians(g, ubo, W, H, tight=True)
+    assert np.array_equal(tight["image"], full["image"])
+    assert 0 < tight["K"] < full["K"]
+    pf = set(zip((full["keys"] >> np.uint64(32)).tolist(), full["vals"].tolist()))
+    pt = set(zip((tight["keys"] >> np.uint64(32)).tolist(), tight["vals"].tolist()))
+    assert pt <= pf
+    gx = (W + 15) // 16
+    ly, lx = np.mgrid[0:16, 0:16]
+    for t, i in pf - pt:
+        px, py = (t % gx) * 16 + lx, (t // gx) * 16 + ly
+        dx = full["means2d"][2 * i].astype(np.float64) - px
+        dy = full["means2d"][2 * i + 1].astype(np.float64) - py
+        co = full["conic"][4 * i:4 * i + 4].astype(np.float64)
+        power = -0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy
+        assert float((co[3] * np.exp(power)).max()) < (1.0 / 255.0) * (1.0 - 1e-4), (t, i)
+    # sorted keys and ranges keep the invariants of the 3-sigma mode
+    keys = tight["keys"]
+    assert np.all(np.diff(keys.astype(np.uint64)) >= 0) and tight["K"] == int(tight["touched"].sum())

@@ -1,0 +1,155 @@
+"""The integer outputs of the frames the headline times. Stream-ordered frames bin
+each Gaussian only to the tiles its alpha >= 1/255 box overlaps (splat.hip gs_preprocess_one, the
+SplatCam::tight branch), not its whole 3-sigma rectangle; the oracle restates that binning
+(oracle_splat_gaussians_tight). PTGS_FLAG_SPLAT_PUBLISH_TIGHT makes a published frame bin the same way,
+through the same front ends, so the timed path's sorted keys / values / tile ranges (and radii / tiles
+touched) are compared with the oracle's bit for bit: at the C2 headline (100k Gaussians, 1920x1080,
+Morton copy with ids, fused front end), at C4's 1M Gaussians (large-tile sorts), and over the edge cases
+of the suite (equal depths, tile-size boundaries, thin / faint Gaussians, a close camera). The published
+frame's pair count equals the timed frames' own count and its image equals theirs bit for bit."""
+import numpy as np
+import pytest
+
+import scenes_util as U
+from pathtracer_gaussiansplatting_amd import Camera, make_ubo
+from pathtracer_gaussiansplatting_amd import synthetic as Y
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _read(renderer, ptr, n, dtype):
+    out = np.zeros(n, dtype)
+    if n:
+        renderer.copy_d2h(out, ptr, out.nbytes)
+    return out
+
+
+def _check_tight(g, ubo, W, H, oracle_lib, frames=2, bg=(0.0, 0.0, 0.0), want_fused=None):
+    """Timed frames (stream-ordered, Morton copy with ids) vs published tight frames vs the oracle's
+    tight mode. Returns (K, fused) of the last published frame."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    n = len(g["opacities"])
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H, bg=bg, tight=True)
+    ra = Renderer(0)
+    rb = Renderer(0, publish_splat_buffers="tight")
+    try:
+        da = ra.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        db = rb.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        timed = []
+        for k in range(frames + 1):
+            out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            ra.splat_gaussians(da, ubo, W, H, out, bg=bg)
+            timed.append(out)
+            torch.cuda.synchronize()  # (frame k's row sizes reach the host before frame k + 1)
+        st_a = ra.splat_status()
+        assert st_a.frames == 0 and st_a.incomplete_tiles == 0
+        assert st_a.last_pairs == ref["K"], (st_a.last_pairs, ref["K"])  # the timed frames' own count
+        fused = []
+        for k in range(frames):  # frame 0: three launches (sizes the rows); then the fused front end
+            pub = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            st = rb.splat_gaussians(db, ubo, W, H, pub, bg=bg, want_stats=True)
+            torch.cuda.synchronize()
+            b = rb.splat_buffers()
+            K = st.num_rendered
+            assert K == ref["K"], (k, K, ref["K"])
+            np.testing.assert_array_equal(_read(rb, b.sorted_keys, K, np.uint64), ref["keys"])
+            np.testing.assert_array_equal(_read(rb, b.sorted_values, K, np.uint32), ref["vals"])
+            np.testing.assert_array_equal(_read(rb, b.tile_ranges, 2 * b.num_tiles, np.uint32), ref["ranges"])
+            np.testing.assert_array_equal(_read(rb, b.radii, n, np.int32), ref["radii"])
+            np.testing.assert_array_equal(_read(rb, b.tiles_touched, n, np.uint32), ref["touched"])
+            assert torch.equal(pub, timed[-1]), f"published tight frame {k} != timed frame"
+            fused.append(st.fused)
+        if want_fused is not None:
+            assert fused[-1] == want_fused, fused
+        err = U.rel_l2(timed[-1].cpu().numpy(), ref["image"])
+        assert err < 1e-4, err
+        return ref["K"], fused[-1]
+    finally:
+        ra.close()
+        rb.close()
+
+
+def test_tight_binning_c2_headline(native_lib, oracle_lib):
+    """C2 exactly as bench.py times it: 100k Gaussians, 1920x1080, the C2 camera, fused front end."""
+    W, H = 1920, 1080
+    g = Y.gaussians_c2(100_000, seed=1)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    K, fused = _check_tight(g, ubo, W, H, oracle_lib, want_fused=1)
+    full = oracle_lib.splat_gaussians(g, ubo, W, H)
+    assert K < full["K"]
+    print(f"C2 timed binning: K {K} of the 3-sigma rectangles' {full['K']}")
+
+
+def test_tight_binning_1m_gaussians(native_lib, oracle_lib):
+    """C4's Gaussian count (1M at 1920x1080): tiles of thousands of pairs, the large-tile radix sort."""
+    W, H = 1920, 1080
+    g = Y.gaussians_c2(1_000_000, seed=3)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    K, _ = _check_tight(g, ubo, W, H, oracle_lib)
+    assert K > 2_000_000, K
+
+
+@pytest.mark.parametrize("case", ["equal_depths", "tile_boundaries", "thin_faint", "close", "orbit"])
+def test_tight_binning_edge_cases(native_lib, oracle_lib, case):
+    W, H, n = 480, 270, 20_000
+    g = Y.gaussians_c2(n, seed=61)
+    eye, at = [0.0, 0.0, 0.0], [0.0, 0.0, -1.0]
+    bg = (0.1, 0.2, 0.3)
+    if case == "equal_depths":
+        g["means"][1::37] = g["means"][0::37][: len(g["means"][1::37])]  # duplicated means: equal depths
+        g["means"][2::41, 2] = g["means"][3::41, 2][: len(g["means"][2::41])]  # equal z only
+    elif case == "tile_boundaries":
+        W, H = 333, 211  # partial tiles at the right and bottom edges
+    elif case == "thin_faint":
+        rng = np.random.default_rng(7)
+        g["scales"] = (g["scales"] * rng.choice([0.05, 1.0, 4.0], size=(n, 3))).astype(np.float32)
+        g["opacities"] = rng.uniform(1e-3, 1.0, size=g["opacities"].shape).astype(np.float32) ** 3
+    elif case == "close":
+        eye, at = [0.0, 0.0, -5.0], [0.3, 0.1, -6.0]  # inside the cloud: Gaussians at the near plane
+    elif case == "orbit":
+        th = np.radians(40.0)
+        eye = [5.0 * np.sin(th), 0.4, -8.0 + 5.0 * np.cos(th)]
+        at = [0.0, 0.0, -8.0]
+    ubo = make_ubo(Camera(aspect=W / H).look_at(eye, at), U.cornell(), 0)
+    _check_tight(g, ubo, W, H, oracle_lib, bg=bg)
+
+
+@pytest.mark.parametrize("mode", ["rects", "tight"])
+def test_band_3_of_8_at_10m_4k_vs_oracle(native_lib, oracle_lib, mode):
+    """the tile-row shard of rank 3 of 8 at C5's splat size (10M Gaussians, 3840x2160),
+    rendered as its own restricted frame (bands over its rows only, chunk bounds, the per-Gaussian row
+    pre-cull): keys / values / ranges / radii / tiles touched equal the oracle's band bit for bit, in both
+    binnings (3-sigma rectangles and the timed frames' alpha boxes)."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    from pathtracer_gaussiansplatting_amd import dist as D
+    W, H, n = 3840, 2160, 10_000_000
+    g = Y.gaussians_c2(n, seed=5)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    rows = D.tile_row_shard(3, 8, H)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H, tile_rows=rows, tight=(mode == "tight"))
+    r = Renderer(0, publish_splat_buffers="tight" if mode == "tight" else True)
+    try:
+        dg = r.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        dgb = dict(dg, chunk_bounds=r.gaussians_chunk_bounds(dg))
+        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        for frame in range(2):  # three launches, then whichever front end the first frame chose
+            st = r.splat_gaussians(dgb, ubo, W, H, out, tile_rows=rows, want_stats=True)
+            torch.cuda.synchronize()
+            b = r.splat_buffers()
+            assert st.num_rendered == ref["K"], (frame, st.num_rendered, ref["K"])
+            np.testing.assert_array_equal(_read(r, b.sorted_keys, ref["K"], np.uint64), ref["keys"])
+            np.testing.assert_array_equal(_read(r, b.sorted_values, ref["K"], np.uint32), ref["vals"])
+            np.testing.assert_array_equal(_read(r, b.tile_ranges, 2 * b.num_tiles, np.uint32), ref["ranges"])
+            np.testing.assert_array_equal(_read(r, b.radii, n, np.int32), ref["radii"])
+            np.testing.assert_array_equal(_read(r, b.tiles_touched, n, np.uint32), ref["touched"])
+        r0, r1 = rows[0] * 16, min(rows[1] * 16, H)
+        err = U.rel_l2(out[r0:r1].cpu().numpy(), ref["image"][r0:r1])
+        assert err < 1e-4, err
+        print(f"10M 4K band {rows}: {ref['K']} pairs ({mode}) bit-exact, rel L2 {err:.2e}")
+    finally:
+        r.close()
