@@ -184,7 +184,9 @@ __device__ __forceinline__ bool gs_row_miss(const SplatCam& cam, float mx, float
 // One Gaussian: frustum cull (d <= 0.2), Sigma = R S^2 R^T, EWA Sigma' = J W Sigma W^T J^T + 0.3,
 // conic, 3-sigma radius, tile rect (returned; empty if culled) and, with STORE, every per-Gaussian
 // output incl. the blend record. (Blocks of other bands recompute the rect without storing.)
-template <bool STORE>
+// ROWCULL: a tile-row-restricted frame (cam.rowcull), its own instantiation of the front-end kernels (the
+// full frame's preprocess keeps its single load round trip, unchanged code)
+template <bool STORE, bool ROWCULL = false>
 __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const PreArgs& A, uint32_t i,
                                                      float* dep_out = nullptr) {
   const float* __restrict__ means = A.means;
@@ -208,7 +210,7 @@ __device__ __forceinline__ ushort4 gs_preprocess_one(const SplatCam& cam, const 
   float sx = scales[3 * i], sy = scales[3 * i + 1], sz = scales[3 * i + 2];
   float qr = 0.0f, qx = 0.0f, qy = 0.0f, qz = 0.0f, op = 0.0f, cr = 0.0f, cg = 0.0f, cbl = 0.0f;
   bool miss = false;
-  if (!cam.rowcull) {
+  if (!ROWCULL) {
     // every input is loaded here, with the id and before the id check and the depth test: one memory round
     // trip per Gaussian (loads behind either branch were issued only once the id / the means had arrived)
     qr = rots[4 * i]; qx = rots[4 * i + 1]; qy = rots[4 * i + 2]; qz = rots[4 * i + 3];
@@ -444,7 +446,7 @@ __global__ __launch_bounds__(256) void gs_chunk_cull_kernel(SplatCam cam, const 
 #ifndef GS_COUNT_THREADS
 #define GS_COUNT_THREADS 1024  // the count's workgroup (the scatter keeps GS_BIN_THREADS)
 #endif
-#define GS_MAX_CHUNKS 256    // colscan: 4 waves x 64 chunks
+#define GS_MAX_CHUNKS 1024   // colscan: 16 waves x up to 64 chunks each
 #ifndef GS_CHUNK_MIN
 #define GS_CHUNK_MIN 512     // Gaussians per chunk (at least)
 #endif
@@ -647,6 +649,7 @@ __device__ __forceinline__ void gs_store_chunk_rect(uint32_t bx0, uint32_t by0, 
 }
 
 // preprocess + count. Block (0, 0) also re-arms the frame's counters.
+template <bool ROWCULL>
 __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                       uint32_t* __restrict__ hist,
                                                                       uint32_t* __restrict__ total,
@@ -680,7 +683,8 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
     // (tile-row shard with chunk bounds: a 256-Gaussian chunk whose bound misses the rows is skipped
     // before its Gaussians are loaded; a wave's 64 lie in at most two chunks)
     const bool skip = cam.cull && i < b1 && A.cskip[i >> 8];
-    if (i < b1 && !skip) rc = blockIdx.x == 0 ? gs_preprocess_one<true>(cam, A, i) : gs_preprocess_one<false>(cam, A, i);
+    if (i < b1 && !skip)
+      rc = blockIdx.x == 0 ? gs_preprocess_one<true, ROWCULL>(cam, A, i) : gs_preprocess_one<false, ROWCULL>(cam, A, i);
     else if (i < b1 && blockIdx.x == 0) gs_store_skipped(A, i);
     uint32_t xw, yh;
     gs_clip(rc, ty0, ty1, xw, yh);
@@ -727,6 +731,8 @@ __global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam
 #define GS_COLSCAN_WAVES 16
 #endif
 #define GS_COLSCAN_THREADS (64 * GS_COLSCAN_WAVES)
+#define GS_CS_REG 16u  // chunk rows per colscan wave kept in registers
+static_assert(GS_MAX_CHUNKS <= GS_COLSCAN_WAVES * 64, "colscan: at most 64 chunk rows per wave");
 __global__ __launch_bounds__(GS_COLSCAN_THREADS) void gs_bin_colscan_kernel(BinGrid bg, uint32_t* __restrict__ hist,
                                                              uint2* __restrict__ tile_info,
                                                              uint32_t* __restrict__ group_total,
@@ -739,24 +745,44 @@ __global__ __launch_bounds__(GS_COLSCAN_THREADS) void gs_bin_colscan_kernel(BinG
   const bool ok = t < bg.row1 * bg.grid_x;
   const uint32_t cpw = (bg.chunks + GS_COLSCAN_WAVES - 1u) / GS_COLSCAN_WAVES, c0 = wave * cpw,
                  c1 = min(bg.chunks, c0 + cpw);
-  // all of this wave's rows in flight at once (cpw <= 64: registers, fully unrolled)
-  uint32_t h[GS_MAX_CHUNKS / GS_COLSCAN_WAVES];
+  // the wave's first GS_CS_REG rows in flight at once and kept in registers (fully unrolled: every
+  // frame of up to 256 chunks); rows beyond them (more chunks: 10M Gaussians at 4K, single-band tile-row
+  // shards of large sets) in batches of GS_CS_REG, read again for the rewrite
+  uint32_t h[GS_CS_REG];
   uint32_t sum = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < GS_MAX_CHUNKS / GS_COLSCAN_WAVES; ++k) {
+  for (uint32_t k = 0; k < GS_CS_REG; ++k) {
     h[k] = (ok && c0 + k < c1) ? hist[(size_t)(c0 + k) * bg.tiles + t] : 0u;
     sum += h[k];
+  }
+  for (uint32_t k0 = GS_CS_REG; k0 < cpw; k0 += GS_CS_REG) {
+    uint32_t x[GS_CS_REG];
+#pragma unroll
+    for (uint32_t k = 0; k < GS_CS_REG; ++k) x[k] = (ok && c0 + k0 + k < c1) ? hist[(size_t)(c0 + k0 + k) * bg.tiles + t] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < GS_CS_REG; ++k) sum += x[k];
   }
   s_ws[wave][lane] = sum;
   __syncthreads();
   uint32_t run = 0;
   for (uint32_t w = 0; w < wave; ++w) run += s_ws[w][lane];
 #pragma unroll
-  for (uint32_t k = 0; k < GS_MAX_CHUNKS / GS_COLSCAN_WAVES; ++k)
+  for (uint32_t k = 0; k < GS_CS_REG; ++k)
     if (ok && c0 + k < c1) {
       hist[(size_t)(c0 + k) * bg.tiles + t] = run;
       run += h[k];
     }
+  for (uint32_t k0 = GS_CS_REG; k0 < cpw; k0 += GS_CS_REG) {
+    uint32_t x[GS_CS_REG];
+#pragma unroll
+    for (uint32_t k = 0; k < GS_CS_REG; ++k) x[k] = (ok && c0 + k0 + k < c1) ? hist[(size_t)(c0 + k0 + k) * bg.tiles + t] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < GS_CS_REG; ++k)
+      if (ok && c0 + k0 + k < c1) {
+        hist[(size_t)(c0 + k0 + k) * bg.tiles + t] = run;
+        run += x[k];
+      }
+  }
   if (wave != 0) return;
   uint32_t tot = 0;
 #pragma unroll
@@ -1009,6 +1035,7 @@ static_assert(GS_FUSED_SLICE <= (uint32_t)GS_FUSED_WG * GS_FUSED_QREG, "a slice'
 static_assert(GS_FUSED_THREADS == 256, "the fused chunk is the chunk-bounds granule (256 Gaussians)");
 
 
+template <bool ROWCULL>
 __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                          uint32_t scap,
                                                                          uint32_t* __restrict__ cursor,
@@ -1100,7 +1127,21 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
     // Gaussians are loaded; it goes through the rest with no pairs)
     const bool skip = cam.cull && (A.cbounds ? gs_chunk_misses(cam, A.cbounds[2 * chunk], A.cbounds[2 * chunk + 1])
                                              : A.cskip[chunk] != 0);
-    if (own && !skip) rc = store ? gs_preprocess_one<true>(cam, A, i, &d) : gs_preprocess_one<false>(cam, A, i, &d);
+    if (owner && skip) {
+      // a culled chunk leaves at once (a tile-row shard of a large set culls most of its ~N / 256
+      // workgroups): what it owes is the empty chunk rect (gs_spill_tile then never reads its Gaussians),
+      // its published zeros, its arrival at the slice queue's owner count and zero partials
+      if (own && store) gs_store_skipped(A, i);
+      if (threadIdx.x == 0) {
+        crect[wg] = make_ushort4(1, 1, 0, 0);
+        atomicAdd(fz + GS_FSQ_W + 2, 1u);
+        fzp[2 * wg] = 0;
+        fzp[2 * wg + 1] = 0;
+      }
+      return;
+    }
+    if (own && !skip)
+      rc = store ? gs_preprocess_one<true, ROWCULL>(cam, A, i, &d) : gs_preprocess_one<false, ROWCULL>(cam, A, i, &d);
     else if (own && store) gs_store_skipped(A, i);
     if (own && store) {  // for gs_spill_tile: the rect (empty: culled) and depth in walk order
       rects_out[i] = rc;
@@ -1741,7 +1782,11 @@ __device__ const uint32_t* gs_spill_tile(const GsSpill& sp, uint32_t tx, uint32_
 //           test_raster_gpu.py); front to back, stop before the Gaussian that would take T below 1e-4
 //           (the reference's rule).
 // OVER (hybrid composite): per-pixel depth limit and an "under" image instead of the background colour
-// Measured and rejected here (git history: round 4): records read by one lane and broadcast with
+// Measured and rejected here: per-4x4-sub-block lists, one per ds_read_b128 lane group of a wave (each
+// group reads its own list's record in the cycle a broadcast takes, 16% fewer evaluation steps at C2):
+// 0.0596 vs 0.0564 ms, the u16 lists' unpacking, four ballots per compaction round and the sub-block
+// masks cost more than the steps saved (the machinery alone with quadrant lists: 0.0620 ms); and (git
+// history: round 4) records read by one lane and broadcast with
 // readfirstlane (C2 0.0784 vs 0.0565 ms), alphas of several entries computed ahead of the transmittance
 // chain, the termination applied without its wave-uniform branch, an XCD-aware tile mapping, loading the
 // key row only up to the previous frame's count, non-temporal records / key rows.
@@ -2266,8 +2311,15 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   bgrid.groups = std::max(1u, (brows * cam.grid_x + 63u) / 64u);
   bgrid.band_rows = std::max(1u, std::min(std::max(brows, 1u), GS_BAND_TILES / cam.grid_x));
   bgrid.bands = std::max(1u, (brows + bgrid.band_rows - 1) / bgrid.band_rows);
-  bgrid.chunks = std::max(1u, std::min({(uint32_t)GS_MAX_CHUNKS, (n + GS_CHUNK_MIN - 1) / GS_CHUNK_MIN,
-                                        std::max(1u, 256u / bgrid.bands)}));
+  // Chunks: the count / scatter walks are latency-bound loops over a chunk's Gaussians, while every chunk
+  // writes (count), scans (colscan) and reads (scatter) a histogram row of its band's tiles. So 256
+  // workgroups in all as long as the rows cost about as much as the walks; beyond that (at least twice
+  // as many Gaussians per chunk as band tiles: 10M at 4K, a single-band tile-row shard of it) up to
+  // GS_MAX_CHUNKS (10M at 4K: front end 4.3 -> 2.9 ms; 1M at 1080p with 1 024 chunks: 0.289 -> 0.330 ms).
+  const uint32_t band_tiles = bgrid.band_rows * cam.grid_x;
+  const uint32_t want_chunks = std::max(256u / bgrid.bands, (uint32_t)std::min<uint64_t>(GS_MAX_CHUNKS, n / std::max(1u, band_tiles / 2u)));
+  bgrid.chunks = std::max(1u, std::min({(uint32_t)GS_MAX_CHUNKS / bgrid.bands, (n + GS_CHUNK_MIN - 1) / GS_CHUNK_MIN,
+                                        want_chunks}));
   bgrid.chunk = std::max(1u, (n + bgrid.chunks - 1) / bgrid.chunks);
   const size_t band_lds = (size_t)bgrid.band_rows * cam.grid_x * 4;
   if ((e = ensure(w->hist, (size_t)bgrid.chunks * tiles * 4))) return e;
@@ -2516,7 +2568,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     BinGrid fg = bgrid;
     fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
     fg.chunk = GS_FUSED_THREADS;
-    hipLaunchKernelGGL(gs_bin_fused_kernel, dim3(fg.bands, fg.chunks + helpers + (order ? 1u : 0u)),
+    hipLaunchKernelGGL(cam.rowcull ? gs_bin_fused_kernel<true> : gs_bin_fused_kernel<false>,
+                       dim3(fg.bands, fg.chunks + helpers + (order ? 1u : 0u)),
                        dim3(GS_FUSED_WG), band_lds, s,
                        cam, fpa, fg, scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
                        (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, order,
@@ -2598,7 +2651,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e2 = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e2;
     if ((e2 = cull_flags())) return e2;
     // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
-    hipLaunchKernelGGL(gs_bin_count_kernel, dim3(bgrid.bands, bgrid.chunks + (order ? 1u : 0u)), dim3(GS_COUNT_THREADS),
+    hipLaunchKernelGGL(cam.rowcull ? gs_bin_count_kernel<true> : gs_bin_count_kernel<false>,
+                       dim3(bgrid.bands, bgrid.chunks + (order ? 1u : 0u)), dim3(GS_COUNT_THREADS),
                        std::max(band_lds, (size_t)GS_ORDER_BUCKETS * 4), s, cam, pa, bgrid, (uint32_t*)w->hist.p,
                        (uint32_t*)w->total.p, (uint32_t*)w->large_ctr.p, w->k_dev, (uint32_t*)w->nzbuf.p,
                        (const uint2*)w->ranges.p, order, cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x,
