@@ -470,6 +470,48 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 // The bands cover the frame's tile rows [row0, row1) only (a tile-row shard bins its own rows: one band of
 // up to GS_MAX_CHUNKS chunks instead of the whole frame's bands); the 64-tile groups start at row0's first
 // tile. hist, tile_info and ranges keep the frame's global tile ids (tiles = grid_x * grid_y).
+// Wave64 min / max / sum in DPP (the scan pattern of wave_incl_scan: lane 63 ends with the reduction of
+// all 64) and broadcast from lane 63: six VALU steps with no LDS round trip, where the __shfl_xor
+// butterfly is six dependent ds_bpermute round trips.
+template <int OP>  // 0 min, 1 max, 2 sum
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t x) {
+  const int id = OP == 0 ? -1 : 0;  // (0xFFFFFFFF: the identity of an unsigned min)
+  auto f = [](uint32_t a, uint32_t b) { return OP == 0 ? min(a, b) : OP == 1 ? max(a, b) : a + b; };
+  x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x111, 0xF, 0xF, false));  // row_shr:1
+  x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x112, 0xF, 0xF, false));  // row_shr:2
+  x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x114, 0xF, 0xF, false));  // row_shr:4
+  x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x118, 0xF, 0xF, false));  // row_shr:8
+  x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  x = f(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// x of lane ^ J without LDS: DPP inside rows of 16 (quad_perm for 1 / 2; half-row / row mirrors composed
+// with them for 4 / 8) and the gfx950 permlane swaps across rows (16) and halves (32)
+template <uint32_t J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x, uint32_t lane) {
+  if (J == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+  if (J == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+  if (J == 4) {  // (i ^ 7) ^ 3
+    const int t = __builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x1B, 0xF, 0xF, false);     // quad_perm 3,2,1,0
+  }
+  if (J == 8) {  // (i ^ 15) ^ 7
+    const int t = __builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x141, 0xF, 0xF, false);    // row_half_mirror
+  }
+  if (J == 16) {  // odd rows of the first result, even rows of the second
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return ((lane >> 4) & 1u) ? r[0] : r[1];
+  }
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // J == 32
+  return lane >= 32u ? r[0] : r[1];
+}
+template <uint32_t J>
+__device__ __forceinline__ unsigned long long lane_xor64(unsigned long long x, uint32_t lane) {
+  return ((unsigned long long)lane_xor<J>((uint32_t)(x >> 32), lane) << 32) | lane_xor<J>((uint32_t)x, lane);
+}
+
 struct BinGrid {
   uint32_t band_rows, bands, chunks, chunk, grid_x, grid_y, tiles, groups, row0, row1;
 };
@@ -579,6 +621,7 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
 // ramp-down runs light tiles only. Any permutation renders the same image: the previous frame's
 // counts (ranges[t].y - .x, whatever path wrote them) only steer the schedule.
 #define GS_ORDER_BUCKETS 256u
+#define GS_ORDER_B 4u  // previous tile counts in flight per work-item (16: 104 VGPRs in the front-end kernels)
 // (order[b] = the tile. Carrying the previous frame's count of the tile in the word, so the blend loads
 // only that much of the key row with the tile, measured slower: C2 0.0594 vs 0.0588 ms)
 __device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
@@ -587,10 +630,23 @@ __device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
 }
 __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restrict__ order, uint32_t tb, uint32_t te,
                               uint32_t* s_h /* >= GS_ORDER_BUCKETS */) {
+  // (the previous counts are loaded GS_ORDER_B per work-item at a time, all in flight before the first
+  // is used: a loop of one load and one LDS atomic per iteration waited for every load, 16 dependent
+  // round trips per pass at 1080p on the front end's critical path)
   const uint32_t tid = threadIdx.x, lane = tid & 63u, nth = blockDim.x;  // (>= 64)
   for (uint32_t b = tid; b < GS_ORDER_BUCKETS; b += nth) s_h[b] = 0;
   __syncthreads();
-  for (uint32_t t = tb + tid; t < te; t += nth) atomicAdd(s_h + gs_order_bucket(prev[t]), 1u);
+  for (uint32_t t0 = tb + tid; t0 < te; t0 += GS_ORDER_B * nth) {
+    uint32_t bk[GS_ORDER_B];
+#pragma unroll
+    for (uint32_t j = 0; j < GS_ORDER_B; ++j) {
+      const uint32_t t = t0 + j * nth;
+      bk[j] = t < te ? gs_order_bucket(prev[t]) : GS_ORDER_BUCKETS;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < GS_ORDER_B; ++j)
+      if (bk[j] < GS_ORDER_BUCKETS) atomicAdd(s_h + bk[j], 1u);
+  }
   __syncthreads();
   if (tid < 64) {  // exclusive scan of the buckets: one wave, four per lane
     const uint32_t c0 = s_h[4 * lane], c1 = s_h[4 * lane + 1], c2 = s_h[4 * lane + 2], c3 = s_h[4 * lane + 3];
@@ -602,7 +658,17 @@ __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restri
     s_h[4 * lane + 3] = ex + c0 + c1 + c2;
   }
   __syncthreads();
-  for (uint32_t t = tb + tid; t < te; t += nth) order[atomicAdd(s_h + gs_order_bucket(prev[t]), 1u)] = t;
+  for (uint32_t t0 = tb + tid; t0 < te; t0 += GS_ORDER_B * nth) {
+    uint32_t bk[GS_ORDER_B];
+#pragma unroll
+    for (uint32_t j = 0; j < GS_ORDER_B; ++j) {
+      const uint32_t t = t0 + j * nth;
+      bk[j] = t < te ? gs_order_bucket(prev[t]) : GS_ORDER_BUCKETS;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < GS_ORDER_B; ++j)
+      if (bk[j] < GS_ORDER_BUCKETS) order[atomicAdd(s_h + bk[j], 1u)] = t0 + j * nth;
+  }
 }
 
 // Spill accounting (see gs_spill_tile), run by the first front-end launch's block (0, 0): the previous
@@ -650,7 +716,7 @@ __device__ __forceinline__ void gs_store_chunk_rect(uint32_t bx0, uint32_t by0, 
 
 // preprocess + count. Block (0, 0) also re-arms the frame's counters.
 template <bool ROWCULL>
-__global__ __launch_bounds__(GS_COUNT_THREADS) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
+__global__ __launch_bounds__(GS_COUNT_THREADS, 4) void gs_bin_count_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                       uint32_t* __restrict__ hist,
                                                                       uint32_t* __restrict__ total,
                                                                       uint32_t* __restrict__ large_ctr,
@@ -1159,12 +1225,10 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
       by0 = yh & 0xFFFFu;
       by1 = by0 + (yh >> 16);
     }
-    for (int off = 32; off > 0; off >>= 1) {
-      bx0 = min(bx0, (uint32_t)__shfl_xor((int)bx0, off));
-      by0 = min(by0, (uint32_t)__shfl_xor((int)by0, off));
-      bx1 = max(bx1, (uint32_t)__shfl_xor((int)bx1, off));
-      by1 = max(by1, (uint32_t)__shfl_xor((int)by1, off));
-    }
+    bx0 = wave_reduce<0>(bx0);
+    by0 = wave_reduce<0>(by0);
+    bx1 = wave_reduce<1>(bx1);
+    by1 = wave_reduce<1>(by1);
     // the rects and the inclusive scan of their areas for the workgroup walk: the per-wave partials of
     // both (rect bounds, area totals) meet behind one barrier
     const uint32_t area = yh ? (xw >> 16) * (yh >> 16) : 0u;
@@ -1308,10 +1372,8 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
       slice = next;
     }
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    acc_pairs += (uint32_t)__shfl_xor((int)acc_pairs, off);
-    acc_res += (uint32_t)__shfl_xor((int)acc_res, off);
-  }
+  acc_pairs = wave_reduce<2>(acc_pairs);
+  acc_res = wave_reduce<2>(acc_res);
   __syncthreads();
   if (lane == 0) {
     s_red[0][wave] = acc_pairs;
@@ -1633,16 +1695,49 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
 // plus, for every other run, the count of that run's keys below it (a binary search of 7 LDS reads):
 // ~200 VALU per key for 2-4 runs and ~400 for 8 instead of n / 4 compares against every key (the
 // counting below): keys are unique, so the ranks are the same.
+// (the exchanges through DPP and the gfx950 permlane swaps: no LDS round trip per step)
+template <uint32_t K, uint32_t J>
+__device__ __forceinline__ unsigned long long gs_sort_step(unsigned long long x, uint32_t lane) {
+  const unsigned long long y = lane_xor64<J>(x, lane);
+  const bool asc = (lane & K) == 0u, low = (lane & J) == 0u;
+  return (asc == low) ? (y < x ? y : x) : (y < x ? x : y);
+}
 __device__ __forceinline__ unsigned long long gs_wave_sort64(unsigned long long x, uint32_t lane) {
-#pragma unroll
-  for (uint32_t k = 2; k <= 64; k <<= 1)
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const unsigned long long y = __shfl_xor(x, (int)j);
-      const bool asc = (lane & k) == 0u, low = (lane & j) == 0u;
-      x = (asc == low) ? (y < x ? y : x) : (y < x ? x : y);
-    }
+  x = gs_sort_step<2, 1>(x, lane);
+  x = gs_sort_step<4, 2>(x, lane); x = gs_sort_step<4, 1>(x, lane);
+  x = gs_sort_step<8, 4>(x, lane); x = gs_sort_step<8, 2>(x, lane); x = gs_sort_step<8, 1>(x, lane);
+  x = gs_sort_step<16, 8>(x, lane); x = gs_sort_step<16, 4>(x, lane); x = gs_sort_step<16, 2>(x, lane);
+  x = gs_sort_step<16, 1>(x, lane);
+  x = gs_sort_step<32, 16>(x, lane); x = gs_sort_step<32, 8>(x, lane); x = gs_sort_step<32, 4>(x, lane);
+  x = gs_sort_step<32, 2>(x, lane); x = gs_sort_step<32, 1>(x, lane);
+  x = gs_sort_step<64, 32>(x, lane); x = gs_sort_step<64, 16>(x, lane); x = gs_sort_step<64, 8>(x, lane);
+  x = gs_sort_step<64, 4>(x, lane); x = gs_sort_step<64, 2>(x, lane); x = gs_sort_step<64, 1>(x, lane);
   return x;
+}
+// keys below x in the sorted 64-key runs [0, m) of s_key except run `self` (m <= R): the binary searches
+// of every run advance in lockstep, so each step's R LDS reads are in flight together (one round trip
+// per step instead of one per step and run); runs >= m are read but not counted
+template <uint32_t R>
+__device__ __forceinline__ uint32_t gs_runs_below(const unsigned long long* s_key, uint32_t m, uint32_t self,
+                                                  unsigned long long x) {
+  uint32_t pos[R];
+#pragma unroll
+  for (uint32_t q = 0; q < R; ++q) pos[q] = 0;
+#pragma unroll
+  for (uint32_t step = 32; step; step >>= 1) {
+    unsigned long long v[R];
+#pragma unroll
+    for (uint32_t q = 0; q < R; ++q) v[q] = s_key[64u * q + pos[q] + step - 1u];
+#pragma unroll
+    for (uint32_t q = 0; q < R; ++q) pos[q] += (q < m && q != self && v[q] < x) ? step : 0u;
+  }
+  uint32_t r = 0;
+  unsigned long long v[R];
+#pragma unroll
+  for (uint32_t q = 0; q < R; ++q) v[q] = s_key[64u * q + pos[q]];
+#pragma unroll
+  for (uint32_t q = 0; q < R; ++q) r += (q < m && q != self) ? pos[q] + (v[q] < x ? 1u : 0u) : 0u;
+  return r;
 }
 // keys of the sorted 64-key run b below x
 __device__ __forceinline__ uint32_t gs_run_below(const unsigned long long* b, unsigned long long x) {
@@ -1982,10 +2077,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     }
     __syncthreads();
     uint32_t r = lane;
-    if (wave < m) {
-      for (uint32_t q = 0; q < m; ++q)
-        if (q != wave) r += gs_run_below(s_key + 64u * q, sk);
-    }
+    if (wave < m) r += gs_runs_below<GS_BLOCK / 64>(s_key, m, wave, sk);
     __syncthreads();  // every read of the keys is done before records overwrite them
     if (tid < n) s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, true);
     if (sk != ~0ull) {
@@ -2041,7 +2133,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         s_key[tid + GS_BLOCK] = k1;
         __syncthreads();
         uint32_t r0 = lane, r1 = lane;
-        for (uint32_t q = 0; q < m; ++q) {
+        for (uint32_t q = 0; q < m; ++q) {  // (8 runs in lockstep for two keys would spill at 64 VGPRs)
           const unsigned long long* run = s_key + 64u * q;
           if (q != wave) r0 += gs_run_below(run, k0);
           if (q != wave + 4u && wave + 4u < m) r1 += gs_run_below(run, k1);
