@@ -72,7 +72,34 @@ static bool collapse_fit(const std::vector<float>& n2, std::vector<float>& n4, u
 // a scene whose 3-triangle-leaf tree is too deep for a 4-wide collapse is rebuilt with 4-triangle
 // leaves before the fan-out is narrowed (a 2-wide fallback traced C5 at 1.38 Grays/s, the
 // 4-triangle-leaf 4-wide tree at ~2.1; with the stack overflow C5 keeps 3-triangle leaves: need 40)
-static const int kBvhTries[][2] = {{PTGS_BVH_LEAF, 4}, {PTGS_BVH_LEAF + 1, 4}, {PTGS_BVH_LEAF, 3}, {PTGS_BVH_LEAF, 2}};
+// Each try also carries the SAH build's depth budget (bvh.cpp: past it, balanced splits).
+struct BvhTry {
+  int leaf, fan;
+  uint32_t depth;
+};
+static const BvhTry kBvhTriesDefault[] = {{PTGS_BVH_LEAF, 4, PTGS_STACK - 1}, {PTGS_BVH_LEAF + 1, 4, PTGS_STACK - 1},
+                                          {PTGS_BVH_LEAF, 3, PTGS_STACK - 1}, {PTGS_BVH_LEAF, 2, PTGS_STACK - 1}};
+// PTGS_BVH_TRIES="leaf:fan:depth,..." replaces the list (A/B of tree shapes: tools/ab_pt.py AB_SCENE=c5)
+static std::vector<BvhTry> bvh_tries() {
+  std::vector<BvhTry> v;
+  if (const char* e = getenv("PTGS_BVH_TRIES")) {
+    for (const char* p = e; *p;) {
+      int l = 0, f = 0;
+      unsigned d = 0;
+      if (sscanf(p, "%d:%d:%u", &l, &f, &d) == 3 && l >= 1 && l <= 16 && f >= 2 && f <= 4 && d >= 1 && d < PTGS_STACK)
+        v.push_back({l, f, d});
+      while (*p && *p != ',') ++p;
+      if (*p == ',') ++p;
+    }
+  }
+  if (v.empty()) v.assign(std::begin(kBvhTriesDefault), std::end(kBvhTriesDefault));
+  return v;
+}
+static void bvh_log(const char* how, int leaf, int fan, uint32_t budget, uint32_t depth, uint32_t need) {
+  if (getenv("PTGS_BVH_LOG"))
+    fprintf(stderr, "[ptgs] %s tree: leaf %d fan %d depth budget %u -> depth %u, stack need %u%s\n", how, leaf, fan,
+            budget, depth, need, need >= PTGS_STACK ? (need < PTGS_STACK_TOTAL ? " (DEEP)" : " (does not fit)") : "");
+}
 
 int fail(ptgs_ctx* c, int code, const char* fmt, ...) {
   char buf[512];
@@ -331,13 +358,16 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     hipError_t e = hipSuccess;
     // (leaf, fan) as the host path (kBvhTries); the LBVH has fixed leaves: fan-out 4, 3, 2
     const bool lbvh = (c->flags & PTGS_FLAG_GPU_LBVH) != 0;
-    const int tries = lbvh ? 3 : (int)(sizeof(kBvhTries) / sizeof(kBvhTries[0]));
+    const std::vector<BvhTry> tl = bvh_tries();
+    const int tries = lbvh ? 3 : (int)tl.size();
     int built_leaf = -1;
+    uint32_t built_depth = 0;
     float4* n4 = nullptr;
     uint32_t num4 = 0, need = PTGS_STACK_TOTAL, dep4 = 0;
     for (int k = 0; k < tries; ++k) {
-      const int leaf = lbvh ? 0 : kBvhTries[k][0], fan = lbvh ? 4 - k : kBvhTries[k][1];
-      if (leaf != built_leaf) {  // (re)build the BVH2
+      const int leaf = lbvh ? 0 : tl[k].leaf, fan = lbvh ? 4 - k : tl[k].fan;
+      const uint32_t depth = lbvh ? PTGS_STACK - 1 : tl[k].depth;
+      if (leaf != built_leaf || depth != built_depth) {  // (re)build the BVH2
         if (built_leaf >= 0) {
           (void)hipFree(g.nodes);
           (void)hipFree(g.tris);
@@ -345,10 +375,11 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
           g = GpuBvh{};
         }
         float bms = 0.0f;
-        e = lbvh ? build_bvh_gpu(tris, PTGS_STACK - 1, g, &bms) : build_bvh_sah_gpu(tris, leaf, PTGS_STACK - 1, g, &bms);
+        e = lbvh ? build_bvh_gpu(tris, PTGS_STACK - 1, g, &bms) : build_bvh_sah_gpu(tris, leaf, depth, g, &bms);
         ms += bms;
         if (e != hipSuccess) break;
         built_leaf = leaf;
+        built_depth = depth;
       }
       // 4-wide collapse on the GPU
       auto t0 = std::chrono::steady_clock::now();
@@ -356,6 +387,7 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
       n4 = nullptr;
       e = collapse_bvh4_gpu(g.nodes, g.num_nodes, fan, &n4, &num4, &need, &dep4);
       auto t1 = std::chrono::steady_clock::now();
+      if (e == hipSuccess) bvh_log("GPU", leaf, fan, depth, dep4, need);
       ms += (float)std::chrono::duration<double, std::milli>(t1 - t0).count();  // build_ms includes it
       if (e != hipSuccess || need < PTGS_STACK_TOTAL) break;
     }
@@ -398,13 +430,17 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     uint32_t num4 = 0, dep4 = 0, need = PTGS_STACK_TOTAL;
     int built_leaf = -1;
     bool fits = false;
-    for (const auto& tr : kBvhTries) {
-      if (tr[0] != built_leaf) {
-        build_bvh(tris, tr[0], PTGS_STACK - 1, bvh);
-        built_leaf = tr[0];
+    uint32_t built_depth = 0;
+    for (const BvhTry& tr : bvh_tries()) {
+      if (tr.leaf != built_leaf || tr.depth != built_depth) {
+        build_bvh(tris, tr.leaf, tr.depth, bvh);
+        built_leaf = tr.leaf;
+        built_depth = tr.depth;
         if (bvh.depth >= PTGS_STACK) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);
       }
-      if ((fits = collapse_fit(bvh.nodes, n4, num4, dep4, tr[1], need))) break;
+      fits = collapse_fit(bvh.nodes, n4, num4, dep4, tr.fan, need);
+      bvh_log("host", tr.leaf, tr.fan, tr.depth, dep4, need);
+      if (fits) break;
     }
     auto t1 = std::chrono::steady_clock::now();
     if (!fits) return fail(c, PTGS_ERANGE, "BVH depth %u exceeds the traversal stack", bvh.depth);

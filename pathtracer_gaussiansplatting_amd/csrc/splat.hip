@@ -1124,7 +1124,12 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
   __shared__ uint32_t s_job[4];  // helpers: (owner, slice) claimed; owners: queue base of their slices
   static_assert(GS_FUSED_THREADS >= GS_ORDER_BUCKETS, "gs_tile_order's buckets live in s_incl");
   if (order && blockIdx.y == gridDim.y - 1) {  // the extra row of blocks: the blend's tile order
-    if (blockIdx.x == 0) gs_tile_order(prev_ranges, order, order_tb, order_te, s_incl);
+    if (blockIdx.x == 0) {
+      STAMP(0, 0);
+      gs_tile_order(prev_ranges, order, order_tb, order_te, s_incl);
+      STAMP_SYNC();
+      STAMP(0, 5);
+    }
     return;
   }
   STAMP(0, 0);
