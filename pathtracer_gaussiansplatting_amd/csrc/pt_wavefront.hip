@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_exte
     // one round of the while-while walk (postponed leaves, as trace_closest)
     while (node >= 0 && node != WF_DONE) {
       Box4 b;
-      box4(r, sc.nodes + 8 * node, h.t, b);
+      box4(r, sc, node, h.t, b);
       if (STATS) tc.nodes += 4;
       if (b.hits == 0) {
         node = pop();
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_shad
     int state = 0;  // 0 running, 1 occluded, 2 unoccluded
     while (node >= 0) {
       Box4 b;
-      box4(r, sc.nodes + 8 * node, r.tmax, b);
+      box4(r, sc, node, r.tmax, b);
       if (STATS) tc.nodes += 4;
       int nxt = -0x7fffffff - 1;
       bool have = false;
