@@ -123,6 +123,13 @@ __device__ __forceinline__ v3 ld3(const float* p) { return mk3(p[0], p[1], p[2])
 #ifndef PTGS_PT_NEARFAR
 #define PTGS_PT_NEARFAR 1
 #endif
+// PTGS_PT_ASM_MIN: the far slab distance's min in inline asm: the compiler canonicalises the hit
+// distance (tcap, a loop-carried value it cannot prove canonical) before every fminf, one VALU per node:
+// C3 at 16 spp 5 380 -> 5 414 Mrays/s (tools/ab_pt.py, profiles/r05/pt_tweaks_ab.log). (Counting the hit
+// children from the sorted distances instead of a running count measured equal: 5 374.)
+#ifndef PTGS_PT_ASM_MIN
+#define PTGS_PT_ASM_MIN 1
+#endif
 
 struct Ray {
   v3 o, d, inv;
@@ -282,7 +289,13 @@ __device__ __forceinline__ void box4(const Ray& r, const DevScene& sc, int node,
     const float y0 = __builtin_fmaf(NY[j], r.inv.y, -r.oinv.y), y1 = __builtin_fmaf(FY[j], r.inv.y, -r.oinv.y);
     const float z0 = __builtin_fmaf(NZ[j], r.inv.z, -r.oinv.z), z1 = __builtin_fmaf(FZ[j], r.inv.z, -r.oinv.z);
     const float tn = fmaxf(fmaxf(x0, y0), fmaxf(z0, r.tmin));
+#if PTGS_PT_ASM_MIN
+    float tf;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf) : "v"(x1), "v"(y1), "v"(z1));
+    asm("v_min_f32 %0, %1, %2" : "=v"(tf) : "v"(tf), "v"(tcap));
+#else
     const float tf = fminf(fminf(x1, y1), fminf(z1, tcap));
+#endif
     const bool h = tn <= tf * 1.0000004f;
     o.tn[j] = h ? tn : __builtin_huge_valf();
     o.c[j] = f2i(CH[j]);
@@ -323,6 +336,17 @@ __device__ __forceinline__ void cswap4(Box4& b, int i, int j) {
   b.tn[i] = sw ? tj : ti; b.tn[j] = sw ? ti : tj;
   b.c[i] = sw ? cj : ci; b.c[j] = sw ? ci : cj;
 }
+// The next node of a closest-hit walk after a 4-wide node test: the nearest hit child, the other hit
+// children pushed farthest first; no hit child: pop().
+template <typename Push, typename Pop>
+__device__ __forceinline__ int enter_box4(Box4& b, Push push, Pop pop) {
+  if (b.hits == 0) return pop();
+  cswap4(b, 0, 1); cswap4(b, 2, 3); cswap4(b, 0, 2); cswap4(b, 1, 3); cswap4(b, 1, 2);
+  if (b.hits > 3) push(b.c[3]);
+  if (b.hits > 2) push(b.c[2]);
+  if (b.hits > 1) push(b.c[1]);
+  return b.c[0];
+}
 
 // SS: the LDS stack's stride (work-items sharing it); OVF: overflow entries beyond the LDS part (0 for
 // a tree whose stack need fits PTGS_STACK: the overflow's branches and scratch cost 3.4% on C3)
@@ -356,15 +380,7 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
       Box4 b;
       box4(r, sc, node, h.t, b);
       if (STATS) cnt.nodes += 4;
-      if (b.hits == 0) {
-        node = pop();
-      } else {
-        cswap4(b, 0, 1); cswap4(b, 2, 3); cswap4(b, 0, 2); cswap4(b, 1, 3); cswap4(b, 1, 2);
-        if (b.hits > 3) push(b.c[3]);
-        if (b.hits > 2) push(b.c[2]);
-        if (b.hits > 1) push(b.c[1]);
-        node = b.c[0];
-      }
+      node = enter_box4(b, push, pop);
       if (node < 0 && leaf == DONE) {
         leaf = node;
         node = pop();

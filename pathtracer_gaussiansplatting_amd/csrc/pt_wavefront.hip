@@ -253,15 +253,7 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_exte
       Box4 b;
       box4(r, sc, node, h.t, b);
       if (STATS) tc.nodes += 4;
-      if (b.hits == 0) {
-        node = pop();
-      } else {
-        cswap4(b, 0, 1); cswap4(b, 2, 3); cswap4(b, 0, 2); cswap4(b, 1, 3); cswap4(b, 1, 2);
-        if (b.hits > 3) push(b.c[3]);
-        if (b.hits > 2) push(b.c[2]);
-        if (b.hits > 1) push(b.c[1]);
-        node = b.c[0];
-      }
+      node = enter_box4(b, push, pop);
       if (node < 0 && leaf == WF_DONE) {
         leaf = node;
         node = pop();
