@@ -64,14 +64,6 @@ struct SplatWorkspace {
   DevBuf dbg_depths, fzp, nzbuf, order;  // order: the blend's tile order (heavy first, fused frames)
   DevBuf crect, sp_keys, sp_vals;  // spilled tiles (gs_spill_tile): chunk rects, the spill pool
   DevBuf fsq;                 // the fused front end's slice queue
-  // position-indexed key rows (GS_POSROWS): fused frame k bins into rows by the schedule position its
-  // blend renders them at, from the tile order (pos_order: position -> tile) and its inverse (pos_of)
-  // that frame k - 1's front end built (set pos_r); frame k builds set 1 - pos_r for frame k + 1. A set
-  // is valid for the tile range it was built for (pos_tb / pos_te); otherwise the frame keeps rows by
-  // tile with the order built in its own front end.
-  DevBuf pos_order[2], pos_of[2];
-  uint32_t pos_tb[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, pos_te[2] = {0u, 0u};
-  uint32_t pos_r = 0;
   DevBuf cskip;               // per 256-Gaussian chunk: skipped by a tile-row-restricted frame
   uint32_t sp_cap = 0;        // spill pool capacity (pairs)
   uint32_t incomplete = 0;    // frames reported incomplete (spill pool exhausted) since the last status clear
@@ -103,8 +95,7 @@ void splat_workspace_destroy(SplatWorkspace* w) {
                    &w->vals_out, &w->ranges, &w->hist, &w->tile_info, &w->group_total, &w->tile_slots, &w->point_keys,
                    &w->total, &w->rect, &w->large, &w->large_ctr, &w->sort_scratch, &w->cursor, &w->fz,
                    &w->pub_offs, &w->keys_pub, &w->vals_pub, &w->dbg_depths, &w->fzp, &w->nzbuf, &w->order,
-                   &w->crect, &w->sp_keys, &w->sp_vals, &w->fsq, &w->cskip, &w->pos_order[0], &w->pos_order[1],
-                   &w->pos_of[0], &w->pos_of[1]};
+                   &w->crect, &w->sp_keys, &w->sp_vals, &w->fsq, &w->cskip};
   for (DevBuf* b : all)
     if (b->p) (void)hipFree(b->p);
   if (w->k_host) (void)hipHostFree(w->k_host);
@@ -638,7 +629,7 @@ __device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
   return GS_ORDER_BUCKETS - 1u - min(GS_ORDER_BUCKETS - 1u, n >> 1);
 }
 __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restrict__ order, uint32_t tb, uint32_t te,
-                              uint32_t* s_h /* >= GS_ORDER_BUCKETS */, uint32_t* __restrict__ pos = nullptr) {
+                              uint32_t* s_h /* >= GS_ORDER_BUCKETS */) {
   // (the previous counts are loaded GS_ORDER_B per work-item at a time, all in flight before the first
   // is used: a loop of one load and one LDS atomic per iteration waited for every load, 16 dependent
   // round trips per pass at 1080p on the front end's critical path)
@@ -676,11 +667,7 @@ __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restri
     }
 #pragma unroll
     for (uint32_t j = 0; j < GS_ORDER_B; ++j)
-      if (bk[j] < GS_ORDER_BUCKETS) {
-        const uint32_t b = atomicAdd(s_h + bk[j], 1u);
-        order[b] = t0 + j * nth;
-        if (pos) pos[t0 + j * nth] = b;  // (position-indexed key rows: the inverse)
-      }
+      if (bk[j] < GS_ORDER_BUCKETS) order[atomicAdd(s_h + bk[j], 1u)] = t0 + j * nth;
   }
 }
 
@@ -1027,7 +1014,6 @@ struct GsFused {  // the sort's and the blend's view of a fused-front-end frame 
   const uint32_t* order;  // blend workgroup -> tile (heavy tiles first; null: row-major)
   uint2* fsq;             // the front end's slice queue (re-armed by block (0, 0): entries and fz[12..14])
   uint32_t fsq_cap;
-  uint32_t posrows;       // key rows and cursors by blend workgroup (schedule position), not by tile
 };
 #ifndef GS_FUSED_WG
 #define GS_FUSED_WG 512  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
@@ -1125,8 +1111,6 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
                                                                          const uint2* __restrict__ prev_ranges,
                                                                          uint32_t* __restrict__ order,
                                                                          uint32_t order_tb, uint32_t order_te,
-                                                                         uint32_t* __restrict__ pos_out,
-                                                                         const uint32_t* __restrict__ pos_in,
                                                                          ushort4* __restrict__ crect,
                                                                          ushort4* __restrict__ rects_out,
                                                                          float* __restrict__ depths_out,
@@ -1142,7 +1126,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
   if (order && blockIdx.y == gridDim.y - 1) {  // the extra row of blocks: the blend's tile order
     if (blockIdx.x == 0) {
       STAMP(0, 0);
-      gs_tile_order(prev_ranges, order, order_tb, order_te, s_incl, pos_out);
+      gs_tile_order(prev_ranges, order, order_tb, order_te, s_incl);
       STAMP_SYNC();
       STAMP(0, 5);
     }
@@ -1284,23 +1268,6 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
     P = (uint32_t)__builtin_amdgcn_readfirstlane((int)P);
     const uint32_t rw = bx1 > bx0 ? bx1 - bx0 : 0u, rh = by1 > by0 ? by1 - by0 : 0u, nt = rw * rh;
     const uint32_t nsl = (P + GS_FUSED_SLICE - 1u) / GS_FUSED_SLICE;  // slices of this chunk (uniform)
-    const float rcp_rw = 1.0f / (float)max(rw, 1u);
-    auto rect_tile = [&](uint32_t k) {  // entry k of the rect's histogram -> its tile
-      uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13 * 2^13: exact after the fix-ups
-      ry = ry * rw > k ? ry - 1 : ry;
-      ry = (ry + 1) * rw <= k ? ry + 1 : ry;
-      return (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
-    };
-    // position-indexed key rows: the rows of the rect's first 4 x GS_FUSED_WG tiles are loaded here,
-    // their latency hidden behind the count walk
-    uint32_t prow[4] = {0u, 0u, 0u, 0u};
-    if (pos_in) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t k = threadIdx.x + j * GS_FUSED_WG;
-        if (k < nt) prow[j] = pos_in[rect_tile(k)];
-      }
-    }
     if (owner) {
       if (threadIdx.x == 0) {  // the workgroup's bounding rect (gs_spill_tile; empty: x0 > x1)
         crect[wg] = nt ? make_ushort4((unsigned short)bx0, (unsigned short)by0, (unsigned short)bx1, (unsigned short)by1)
@@ -1341,22 +1308,25 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
       __syncthreads();
       STAMP(0, 3);
       // reserve: one returning atomic per touched tile (all of a work-item's issued before any is
-      // used); the LDS entry becomes the run's key row and base (row << 12 | min(base, scap))
+      // used); the LDS entry becomes the run's base
+      const float rcp_rw = 1.0f / (float)max(rw, 1u);
       for (uint32_t k0 = threadIdx.x; k0 < nt; k0 += 4 * GS_FUSED_WG) {
         uint32_t c[4], t[4], base[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t k = k0 + j * GS_FUSED_WG;
           c[j] = k < nt ? s_hist[k] : 0u;
-          t[j] = rect_tile(k);
-          if (pos_in) t[j] = k0 == threadIdx.x ? prow[j] : (c[j] ? pos_in[t[j]] : 0u);  // (t: the key row)
+          uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13 * 2^13: exact after the fix-ups
+          ry = ry * rw > k ? ry - 1 : ry;
+          ry = (ry + 1) * rw <= k ? ry + 1 : ry;
+          t[j] = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) base[j] = c[j] ? atomicAdd(cursor + t[j], c[j]) : 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (!c[j]) continue;
-          s_hist[k0 + j * GS_FUSED_WG] = (t[j] << 12) | min(base[j], scap);
+          s_hist[k0 + j * GS_FUSED_WG] = base[j];
           acc_pairs += c[j];
           ++acc_res;
           if (base[j] <= scap && base[j] + c[j] > scap) atomicAdd(fz + 5, 1u);  // (one crossing per spilled tile)
@@ -1371,11 +1341,15 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
 #pragma unroll
       for (uint32_t c = 0; c < GS_FUSED_QREG; ++c) {
         if (c < kept) {
-          const uint32_t v = s_hist[pk[c] & 0x1FFFu], rel = (v & 0xFFFu) + ((pk[c] >> 13) & ((1u << GS_KEEP_RB) - 1u));
+          const uint32_t k = pk[c] & 0x1FFFu, rel = s_hist[k] + ((pk[c] >> 13) & ((1u << GS_KEEP_RB) - 1u));
           const uint4 e = s_e[pk[c] >> (13u + GS_KEEP_RB)];
+          uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13: exact after the fix-ups
+          ry = ry * rw > k ? ry - 1 : ry;
+          ry = (ry + 1) * rw <= k ? ry + 1 : ry;
+          const uint32_t t = (by0 + ry) * bg.grid_x + bx0 + (k - ry * rw);
           if (rel < scap) {
             const unsigned long long key = ((unsigned long long)e.w << 32) | e.z;
-            tile_slots[(size_t)(v >> 12) * scap + rel] = key;
+            tile_slots[(size_t)t * scap + rel] = key;
           }
         }
       }
@@ -1684,9 +1658,8 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
   // static striding over the list (a shared work counter serialises: ~30 ns per contended atomic,
   // 210 us for the 1M-Gaussian frame's 7k claims)
   for (uint32_t li = fu.scap ? 0 : blockIdx.x; li < count; li += fu.scap ? 1 : gridDim.x) {
-    const uint32_t row = fu.scap ? s_list[li] : large[li];  // (fused: the key row; else the tile)
-    const uint32_t tile = (fu.scap && fu.posrows) ? fu.order[row] : row;
-    const uint2 range = fu.scap ? make_uint2(row * fu.scap, row * fu.scap + fu.cursor[row]) : ranges[tile];
+    const uint32_t tile = fu.scap ? s_list[li] : large[li];
+    const uint2 range = fu.scap ? make_uint2(tile * fu.scap, tile * fu.scap + fu.cursor[tile]) : ranges[tile];
     if (!fu.scap && range.y > cap) continue;  // segment beyond the pair buffer: spilled (gs_spill_tile)
     const uint32_t n = range.y - range.x;
     unsigned long long* seg = fu.scap ? const_cast<unsigned long long*>(tile_slots) + range.x
@@ -1921,9 +1894,7 @@ __device__ const uint32_t* gs_spill_tile(const GsSpill& sp, uint32_t tx, uint32_
 #ifndef GS_BLEND_MIN_BLOCKS
 #define GS_BLEND_MIN_BLOCKS 8  // 64 VGPRs: 8 waves per SIMD (vs 7 at 70 VGPRs): +3% at C2
 #endif
-// POS: position-indexed key rows (GsFused::posrows): the row, its count and the workgroup's tile are
-// three independent loads
-template <bool OVER, bool POS>
+template <bool OVER>
 __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_kernel(SplatCam cam, const uint2* __restrict__ ranges,
                                                                  unsigned long long* __restrict__ pairs,
                                                                  uint32_t sorted_above,
@@ -1997,30 +1968,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   }
   uint32_t tile_x = blockIdx.x, tile_y = cam.row_begin + blockIdx.y;
   uint32_t tile = tile_y * cam.grid_x + tile_x;
-  // the tile's key row (loaded together with its count: no dependent round trip for small tiles; every
-  // work-item loads its slot whatever the count). Position-indexed rows (fu.posrows): row b of blend
-  // workgroup b, loaded in parallel with the workgroup's tile (heavy tiles first, gs_tile_order); else
-  // the tile's row, after the tile.
-  const uint32_t srow = fu.scap ? fu.scap : GS_TILE_SLOTS;
-  const uint32_t bidx = blockIdx.y * gridDim.x + blockIdx.x;
-  uint32_t row = bidx, c_row = 0;
-  unsigned long long k_slot = 0;
-  if (POS) {
-    const uint32_t tv = fu.order[bidx];
-    k_slot = tile_slots[(size_t)row * srow + tid];
-    c_row = fu.cursor[row];
-    tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)tv);
+  if (fu.order) {  // heavy tiles first (gs_tile_order)
+    tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)fu.order[blockIdx.y * gridDim.x + blockIdx.x]);
     tile_y = tile / cam.grid_x;
     tile_x = tile - tile_y * cam.grid_x;
-  } else {
-    if (fu.order) {  // heavy tiles first (gs_tile_order)
-      tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)fu.order[bidx]);
-      tile_y = tile / cam.grid_x;
-      tile_x = tile - tile_y * cam.grid_x;
-    }
-    row = tile;
-    k_slot = tile_slots[(size_t)row * srow + tid];
-    if (fu.scap) c_row = fu.cursor[row];
   }
   STAMP(1, 4);
   const float tx0 = (float)(tile_x * GS_BLOCK_X), ty0 = (float)(tile_y * GS_BLOCK_Y);
@@ -2073,9 +2024,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     }
     return qm;
   };
+  // the tile's slot row is loaded together with its count (no dependent round trip for small tiles;
+  // every work-item loads its slot whatever the count)
+  const uint32_t srow = fu.scap ? fu.scap : GS_TILE_SLOTS;
+  const unsigned long long k_slot = tile_slots[(size_t)tile * srow + tid];
   uint2 range;
-  if (POS || fu.scap) {  // (POS: a fused frame)
-    range = make_uint2(row * fu.scap, row * fu.scap + c_row);
+  if (fu.scap) {
+    const uint32_t c = fu.cursor[tile];
+    range = make_uint2(tile * fu.scap, tile * fu.scap + c);
   } else {
     range = ranges[tile];
   }
@@ -2323,7 +2279,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     }
   }
   STAMP(1, 2);
-  if (fu.scap && tid == 0 && n_front) fu.cursor[row] = 0;  // (n > 0: every wave passed a barrier after reading it)
+  if (fu.scap && tid == 0 && n_front) fu.cursor[tile] = 0;  // (n > 0: every wave passed a barrier after reading it)
   if (inside) {
     // the pixel index is recomputed here from a laundered thread id, so that the one computed before
     // the batch loop is not kept (spilled) across it
@@ -2592,11 +2548,6 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   // two in [256, GS_FUSED_MAX_SCAP]); otherwise, or above that capacity, count + colscan + scatter.
 #ifndef GS_FUSED_MAX_SCAP
 #define GS_FUSED_MAX_SCAP 2048u  // larger tiles (1M Gaussians at 1080p): three launches measured faster
-// the fused front end's reservation entries pack (key row << 12 | base clamped to scap)
-static_assert(GS_FUSED_MAX_SCAP < 4096u && (uint64_t)GS_MAX_GROUPS * 64u <= (1u << 20), "reservation entry packing");
-#ifndef GS_POSROWS
-#define GS_POSROWS 1
-#endif
 #endif
 #ifndef GS_FUSED_RUNS_PER_TILE
 #define GS_FUSED_RUNS_PER_TILE 32u  // (C2 Morton order: 6; random order: 51; orbit views up to ~20, where
@@ -2646,8 +2597,7 @@ static_assert(GS_FUSED_MAX_SCAP < 4096u && (uint64_t)GS_MAX_GROUPS * 64u <= (1u 
   };
   auto blend = [&](uint32_t cap, const GsFused& fu, unsigned long long* keys_out, bool sort_large) -> hipError_t {
     if (rows == 0) return hipSuccess;
-    auto k = depth ? (fu.posrows ? gs_sort_blend_kernel<true, true> : gs_sort_blend_kernel<true, false>)
-                   : (fu.posrows ? gs_sort_blend_kernel<false, true> : gs_sort_blend_kernel<false, false>);
+    auto k = depth ? gs_sort_blend_kernel<true> : gs_sort_blend_kernel<false>;
     const dim3 grid(cam.grid_x, rows);
     hipLaunchKernelGGL(k, grid, dim3(GS_BLOCK), 0, s, cam, (const uint2*)w->ranges.p, (unsigned long long*)w->pairs.p,
                        sort_large ? (uint32_t)GS_MID : 0xFFFFFFFFu, keys_out, (uint32_t*)w->vals_out.p,
@@ -2670,7 +2620,7 @@ static_assert(GS_FUSED_MAX_SCAP < 4096u && (uint64_t)GS_MAX_GROUPS * 64u <= (1u 
     if ((e = ensure(w->order, (size_t)tiles * 4))) return e;
     order = (uint32_t*)w->order.p;
   }
-  const GsFused no_fu = {0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order, nullptr, 0u, 0u};
+  const GsFused no_fu = {0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order, nullptr, 0u};
 
   auto enqueue_fused = [&]() -> hipError_t {
     hipError_t e2;
@@ -2703,32 +2653,8 @@ static_assert(GS_FUSED_MAX_SCAP < 4096u && (uint64_t)GS_MAX_GROUPS * 64u <= (1u 
       if ((e2 = hipMemsetAsync(w->fsq.p, 0, w->fsq.bytes, s))) return e2;
     }
     const uint32_t fsq_cap = (uint32_t)std::min<size_t>(w->fsq.bytes / 8, 0x7FFFFFFFu);
-    // the tile order: built by this front end for the next fused frame (set 1 - pos_r, with its inverse);
-    // this frame bins into position-indexed rows when set pos_r holds the order for its tile range, else
-    // into rows by tile with the order being built now (the first frame, a new tile range)
-    const uint32_t tb = cam.row_begin * cam.grid_x, te = cam.row_end * cam.grid_x;
-    uint32_t* ord_next = order;
-    uint32_t* pos_next = nullptr;
-    const uint32_t* pos_cur = nullptr;
-    const uint32_t* ord_cur = nullptr;
-    const uint32_t pr = w->pos_r;
-    if (order && GS_POSROWS) {
-      for (int k = 0; k < 2; ++k) {
-        const void* a = w->pos_order[k].p;
-        const void* b = w->pos_of[k].p;
-        if ((e2 = ensure(w->pos_order[k], (size_t)tiles * 4)) || (e2 = ensure(w->pos_of[k], (size_t)tiles * 4))) return e2;
-        if (a != w->pos_order[k].p || b != w->pos_of[k].p) w->pos_tb[k] = 0xFFFFFFFFu;  // (reallocated: empty)
-      }
-      ord_next = (uint32_t*)w->pos_order[1 - pr].p;
-      pos_next = (uint32_t*)w->pos_of[1 - pr].p;
-      if (w->pos_tb[pr] == tb && w->pos_te[pr] == te) {
-        pos_cur = (const uint32_t*)w->pos_of[pr].p;
-        ord_cur = (const uint32_t*)w->pos_order[pr].p;
-      }
-    }
     GsFused fu = {scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
-                  (uint32_t*)w->fzp.p, nwg, pos_cur ? ord_cur : ord_next, (uint2*)w->fsq.p, fsq_cap,
-                  pos_cur ? 1u : 0u};
+                  (uint32_t*)w->fzp.p, nwg, order, (uint2*)w->fsq.p, fsq_cap};
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers (band 0 stores them for gs_spill_tile)
     if (cam.cull && (n + 255u) / 256u > GS_FUSED_OWN_CULL) {
       if ((e2 = cull_flags())) return e2;
@@ -2743,15 +2669,10 @@ static_assert(GS_FUSED_MAX_SCAP < 4096u && (uint64_t)GS_MAX_GROUPS * 64u <= (1u 
                        dim3(fg.bands, fg.chunks + helpers + (order ? 1u : 0u)),
                        dim3(GS_FUSED_WG), band_lds, s,
                        cam, fpa, fg, scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
-                       (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, ord_next, tb, te, pos_next,
-                       pos_cur, (ushort4*)w->crect.p, (ushort4*)w->rect.p, (float*)w->depths.p, w->k_dev,
-                       (uint2*)w->fsq.p, fsq_cap);
+                       (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, order,
+                       cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x, (ushort4*)w->crect.p, (ushort4*)w->rect.p,
+                       (float*)w->depths.p, w->k_dev, (uint2*)w->fsq.p, fsq_cap);
     if ((e2 = hipGetLastError())) return e2;
-    if (pos_next) {  // the next fused frame bins by the order built here
-      w->pos_tb[1 - pr] = tb;
-      w->pos_te[1 - pr] = te;
-      w->pos_r = 1 - pr;
-    }
     if ((e2 = mark(1)) || (e2 = mark(2)) || (e2 = mark(3))) return e2;
     unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
     const bool sort_large = w->k_host[1] > GS_MID;
@@ -2771,6 +2692,7 @@ static_assert(GS_FUSED_MAX_SCAP < 4096u && (uint64_t)GS_MAX_GROUPS * 64u <= (1u 
       if ((e2 = ensure(w->pub_offs, (size_t)tiles * 4))) return e2;
       if ((e2 = ensure(w->keys_pub, (size_t)tiles * scap * 8))) return e2;  // (K <= tiles * scap)
       if ((e2 = ensure(w->vals_pub, (size_t)tiles * scap * 4))) return e2;
+      const uint32_t tb = cam.row_begin * cam.grid_x, te = cam.row_end * cam.grid_x;
       hipLaunchKernelGGL(gs_publish_scan_kernel, dim3(1), dim3(GS_PUB_THREADS), 0, s, (const uint2*)w->ranges.p, tiles,
                          tb, te, scap, (uint32_t*)w->pub_offs.p);
       hipLaunchKernelGGL(gs_publish_copy_kernel, dim3(tiles), dim3(256), 0, s, (const uint2*)w->ranges.p,

@@ -21,7 +21,7 @@ def main():
     arms = sys.argv[1:] or ["default"]
     spp = int(os.environ.get("AB_SPP", "16"))
     rounds = int(os.environ.get("AB_ROUNDS", "3"))
-    W, H = 3840, 2160
+    W, H = int(os.environ.get("AB_W", "3840")), int(os.environ.get("AB_H", "2160"))  # (C3: 1920 x 1080, AB_TRIS=250000)
     scene = Y.atrium_scene(target_tris=int(os.environ.get("AB_TRIS", "1000000")), seed=2)
     scene.blue_noise = Y.blue_noise(1024)
     pose = Camera(aspect=W / H).look_at([-15.0, 4.0, 5.0], [10.0, 3.0, -3.0])

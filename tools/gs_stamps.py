@@ -85,9 +85,10 @@ def main():
             print(f"  helpers: {len(hs)} stamped, starts {(hs[:, 0].min() - f[:, 0].min()) * 0.01:.2f} .. "
                   f"{(hs[:, 0].max() - f[:, 0].min()) * 0.01:.2f} us")
         print(f"  gap fused end -> first blend start {(b[:, 0].min() - f[:, 5].max()) * 0.01:.2f} us")
-        o = fall[chunks + (len(hs) if len(hs) else 0)]  # the tile-order workgroup (the extra row; no helpers at C2)
-        if o[0] > 0 and o[5] > 0:
-            print(f"  tile-order workgroup: starts {(o[0] - f[:, 0].min()) * 0.01:.2f} us, lasts {(o[5] - o[0]) * 0.01:.2f} us")
+        for o in hs[-1:]:  # the tile-order workgroup (the extra last row; at C2 no helper workgroups launch)
+            if o[5] > 0:
+                print(f"  tile-order workgroup: starts {(o[0] - f[:, 0].min()) * 0.01:.2f} us, ends "
+                      f"{(o[5] - f[:, 0].min()) * 0.01:.2f} us (owners' last end {(f[:, 5].max() - f[:, 0].min()) * 0.01:.2f} us)")
     print(f"blend: {len(b)} workgroups, span {(b[:, 3].max() - b[:, 0].min()) * 0.01:.2f} us, "
           f"last start {(b[:, 0].max() - b[:, 0].min()) * 0.01:.2f} us after the first")
     for k, nm in enumerate(["keys + sort + stage", "evaluation (wave 0)", "tail (slowest wave + store)"]):
