@@ -120,6 +120,30 @@ def test_atrium_250k(pt, oracle_lib):
     print(f"atrium rel L2 {err:.2e}, {nd} pixels differ")
 
 
+@pytest.mark.parametrize("tries", ["4:4:38", "3:3:38", "3:2:38", "2:4:38"])
+def test_tree_shapes_render_the_same_image(pt, oracle_lib, tries, monkeypatch):
+    """The hits do not depend on the tree (closest hit with the lower-id tie rule, padded boxes, the near /
+    far slab test): the C3 scene uploaded with other leaf sizes / fan-outs (api.cpp PTGS_BVH_TRIES, incl.
+    the 2-wide nodes whose empty slots hold point boxes at 1e30) renders bit for bit the default tree's
+    image and the oracle's."""
+    sc = U.atrium()
+    ubo = make_ubo(U.atrium_pose(), sc, 0, ambient=(0.3, 0.4, 0.5, 1.0))
+    monkeypatch.delenv("PTGS_BVH_TRIES", raising=False)
+    g0, s0 = _gpu_render(pt, sc, ubo, 160, 90, 2)
+    info0 = pt.scene_info()
+    monkeypatch.setenv("PTGS_BVH_TRIES", tries)
+    g1, s1 = _gpu_render(pt, sc, ubo, 160, 90, 2)
+    info1 = pt.scene_info()
+    monkeypatch.delenv("PTGS_BVH_TRIES")
+    leaf = int(tries.split(":")[0])
+    assert info1.max_leaf_size <= leaf and (info1.num_bvh_nodes, info1.max_leaf_size) != (info0.num_bvh_nodes,
+                                                                                          info0.max_leaf_size)
+    assert np.array_equal(g0, g1), f"tree {tries}: {int(np.count_nonzero(np.any(g0 != g1, -1)))} pixels differ"
+    assert (s0.extension_rays, s0.shadow_rays) == (s1.extension_rays, s1.shadow_rays)
+    o, so = _oracle_render(oracle_lib, sc, ubo, 160, 90, 2)
+    _compare(g1, o, s1, so)
+
+
 def test_sample_shard_sum_mode(pt, oracle_lib):
     """§8e sample-index shard: rank g of G renders frames g, g+G, ... in SUM mode."""
     sc = U.cornell()
