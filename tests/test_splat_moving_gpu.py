@@ -391,3 +391,37 @@ def test_gaussians_alpha_box_binning_is_exact(native_lib, oracle_lib, shape):
     finally:
         ra.close()
         rb.close()
+
+
+def test_row_gather_pipeline_streams_on_one_gpu(native_lib):
+    """dist.RowGatherPipeline's device path (the bench's multi-rank C2 leg): two images alternate on the
+    compute stream, each frame's gather is issued on a second stream behind an event and the frame two
+    later waits for it. On one GPU without a process group the gather is a no-op, so what is checked is
+    the stream / event plumbing: a moving sequence through the pipeline leaves each image equal, bit for
+    bit, to the same frame rendered directly."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    from pathtracer_gaussiansplatting_amd import dist as D
+    W, H, n = 640, 360, 30_000
+    g = Y.gaussians_c2(n, seed=17)
+    poses = [Camera(aspect=W / H).look_at([0.3 * k, 0.1 * k, -0.4 * k], [0.0, 0.0, -8.0]) for k in range(5)]
+    ubos = [make_ubo(p, U.cornell(), 0) for p in poses]
+    r = Renderer(0)
+    try:
+        dg = r.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        s = torch.cuda.Stream()
+        pipe = D.RowGatherPipeline(r, W, H, [(0, (H + 15) // 16)], 0, 1, stream=s)
+        outs = []
+        with torch.cuda.stream(s):
+            for u in ubos:
+                outs.append(pipe.submit(dg, u))
+            pipe.wait()
+        s.synchronize()
+        got = [outs[-2].clone(), outs[-1].clone()]
+        for img, u in zip(got, ubos[-2:]):
+            ref = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            r.splat_gaussians(dg, u, W, H, ref)
+            torch.cuda.synchronize()
+            assert torch.equal(img, ref)
+        assert outs[-1] is not outs[-2] and outs[-1] is outs[-3]  # two images alternate
+    finally:
+        r.close()
