@@ -28,6 +28,7 @@ FLAG_GPU_LBVH = 32
 FLAG_SPLAT_PUBLISH = 8
 FLAG_PT_WAVEFRONT = 16
 FLAG_SPLAT_PUBLISH_TIGHT = 64  # tests: published frames bin like the stream-ordered (timed) frames
+FLAG_SPLAT_OVERLAP = 128  # frames in flight: a splat call's front end overlaps the previous call's blend
 
 # ---------------------------------------------------------------------------------------------
 # numpy dtypes for the array structs (byte-compatible with Helpers/GeneralHeaders.h)

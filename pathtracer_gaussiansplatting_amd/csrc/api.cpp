@@ -36,6 +36,10 @@
 
 using namespace ptgs;
 
+// frames in flight of PTGS_FLAG_SPLAT_OVERLAP: workspaces in the ring (the front end of call k may run
+// beside the blends of calls k - 1 .. k - RING + 1; PTGS_GS_OV_DEPTH=2 uses two)
+#define PTGS_OV_RING 3
+
 struct ptgs_ctx {
   int device = 0;
   std::string err;
@@ -51,6 +55,15 @@ struct ptgs_ctx {
   SplatWorkspace* view_ws[PTGS_MAX_VIEWS] = {};
   hipStream_t view_stream[PTGS_MAX_VIEWS] = {};
   hipEvent_t view_fork = nullptr, view_join[PTGS_MAX_VIEWS] = {};
+  // PTGS_FLAG_SPLAT_OVERLAP: a ring of workspaces (`splat` is always the latest call's; ov_ring[0] is the
+  // context's own first workspace), the front-end stream, the caller's stream at the start of each of the
+  // last calls (ov_call[i]: the call that used ov_ring[i]), the front end's end
+  SplatWorkspace* ov_ring[PTGS_OV_RING] = {};
+  hipStream_t ov_stream = nullptr;
+  hipEvent_t ov_call[PTGS_OV_RING] = {}, ov_done = nullptr;
+  uint32_t ov_pos = 0;      // ring slot of the latest overlapped call
+  uint32_t ov_depth = 0;    // workspaces in use (2 .. PTGS_OV_RING)
+  uint32_t ov_started = 0;  // consecutive overlapped calls so far (their ov_call events are valid)
   ptgs::WfWorkspace wf;  // wavefront path tracer buffers (PTGS_FLAG_PT_WAVEFRONT)
   ptgs::PtSched pt_sched;  // megakernel tile schedule (heavy tiles first)
   void* comm = nullptr;  // RCCL communicator (ptgs_comm_create)
@@ -94,6 +107,13 @@ static std::vector<BvhTry> bvh_tries() {
   }
   if (v.empty()) v.assign(std::begin(kBvhTriesDefault), std::end(kBvhTriesDefault));
   return v;
+}
+// 4-wide nodes the traversal can address (PTGS_BVH_NODE_LIMIT lowers it: the guard's GPU test)
+static uint32_t bvh_node_limit() {
+  const uint32_t hw = 0x7fffffffu / 128u;
+  const char* e = getenv("PTGS_BVH_NODE_LIMIT");
+  const unsigned long v = e ? strtoul(e, nullptr, 10) : 0ul;
+  return v && v < hw ? (uint32_t)v : hw;
 }
 static void bvh_log(const char* how, int leaf, int fan, uint32_t budget, uint32_t depth, uint32_t need) {
   if (getenv("PTGS_BVH_LOG"))
@@ -188,13 +208,21 @@ void ptgs_destroy(ptgs_ctx* c) {
   if (c->counters) (void)hipFree(c->counters);
   ptgs::wf_workspace_free(c->wf);
   ptgs::free_pt_sched(c->pt_sched);
-  splat_workspace_destroy(c->splat);
+  // (c->splat is one of the ring's workspaces once PTGS_FLAG_SPLAT_OVERLAP has been used: ring slot 0 is
+  // the context's first one, freed here; the others below)
+  splat_workspace_destroy(c->ov_ring[0] ? c->ov_ring[0] : c->splat);
   for (int v = 0; v < PTGS_MAX_VIEWS; ++v) {
     if (c->view_ws[v]) splat_workspace_destroy(c->view_ws[v]);
     if (c->view_stream[v]) (void)hipStreamDestroy(c->view_stream[v]);
     if (c->view_join[v]) (void)hipEventDestroy(c->view_join[v]);
   }
   if (c->view_fork) (void)hipEventDestroy(c->view_fork);
+  for (SplatWorkspace* w : c->ov_ring)  // (ring slot 0 is the context's first workspace: freed above)
+    if (w && w != c->ov_ring[0]) splat_workspace_destroy(w);
+  if (c->ov_stream) (void)hipStreamDestroy(c->ov_stream);
+  for (hipEvent_t ev : c->ov_call)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->ov_done) (void)hipEventDestroy(c->ov_done);
   if (c->comm) (void)comm_destroy(c->comm);
   delete c;
 }
@@ -455,6 +483,12 @@ int ptgs_scene_upload(ptgs_ctx* c, const ptgs_scene_desc* d) {
     c->info.max_leaf_size = bvh.max_leaf;
     c->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   }
+  // The traversal reads 4-wide nodes through a buffer descriptor with 32-bit byte offsets (node << 7,
+  // num_records 0x7fffffff: pt_device.h box4): nodes past 2 GiB would read as zeros (no boxes, child
+  // link 0) without a fault. Such a tree (~16.7M nodes, some 50M triangles) is refused here.
+  if (c->info.num_bvh_nodes > bvh_node_limit())
+    return fail(c, PTGS_ERANGE, "BVH of %u 4-wide nodes exceeds the traversal's 2 GiB node window (%u nodes)",
+                c->info.num_bvh_nodes, bvh_node_limit());
   // a zero vertex/index count still needs valid (never dereferenced) pointers
   ptgs_vertex dummy_v{};
   uint32_t dummy_i = 0;
@@ -666,7 +700,8 @@ extern "C" {
 // caller turns it into PTGS_EINCOMPLETE / PTGS_EINVAL (splat_report) once everything it renders is enqueued.
 static int splat_render(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
                         const float bg[3], const float* depth, const float* under, uint32_t tile_row_begin,
-                        uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream, uint32_t* report) {
+                        uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream, uint32_t* report,
+                        const SplatOverlap* ov = nullptr) {
   *report = 0;
   if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
   if (g->count && (!is_device_ptr(g->means) || !is_device_ptr(g->scales) || !is_device_ptr(g->rotations) ||
@@ -682,7 +717,7 @@ static int splat_render(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
   hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, depth, under,
                                  tile_row_begin, tile_row_end, out, stats, (c->flags & PTGS_FLAG_TIME_STAGES) != 0,
                                  (c->flags & PTGS_FLAG_SPLAT_PUBLISH) != 0, (c->flags & PTGS_FLAG_SPLAT_PUBLISH_TIGHT) != 0,
-                                 (hipStream_t)stream, report);
+                                 (hipStream_t)stream, report, ov);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_gaussians: %s", hipGetErrorString(e));
   return PTGS_OK;
 }
@@ -695,12 +730,82 @@ static int splat_report(ptgs_ctx* c, uint32_t report) {
   return PTGS_OK;
 }
 
+// PTGS_FLAG_SPLAT_OVERLAP: the call takes the other workspace (the one of the call before the previous
+// one) and, for a stream-ordered frame, its front end runs on the context's second stream once the caller's
+// stream has finished what it held at the start of the previous call: that covers the workspace's last
+// frame (two calls ago, blend included) and the inputs the caller wrote before then. Without the flag
+// the front end follows the caller's stream (ov_started is cleared: the next overlapped call starts
+// from the caller's stream as it is then).
+// workspaces in the ring, fixed when a context first overlaps (PTGS_GS_OV_DEPTH=2: two; A/B switch)
+static uint32_t overlap_depth() {
+  const char* v = getenv("PTGS_GS_OV_DEPTH");
+  const int x = v ? atoi(v) : PTGS_OV_RING;
+  return (uint32_t)std::max(2, std::min(x, PTGS_OV_RING));
+}
+
+static int splat_overlap_begin(ptgs_ctx* c, hipStream_t s, SplatOverlap* ov) {
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->ov_ring[0]) {  // the ring starts at the current workspace
+    c->ov_ring[0] = c->splat;
+    c->ov_pos = 0;
+    c->ov_depth = overlap_depth();
+  }
+  const uint32_t depth = c->ov_depth;
+  for (uint32_t i = 1; i < depth; ++i)
+    if (!c->ov_ring[i]) c->ov_ring[i] = splat_workspace_create();
+  if (!c->ov_stream) {
+    // the front end's queue at the highest priority, so its workgroups take the CU slots of the blend's
+    // retiring workgroups early instead of waiting for the blend's tail (PTGS_GS_OV_PRIO=normal: A/B switch)
+    int least = 0, greatest = 0, prio = 0;
+    const char* pv = getenv("PTGS_GS_OV_PRIO");
+    if (!(pv && !strcmp(pv, "normal")) && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      prio = greatest;
+    HIPCHK(c, hipStreamCreateWithPriority(&c->ov_stream, hipStreamNonBlocking, prio));
+  }
+  // (device-scope events: both streams are on this device, so no system-scope release (an L2 write-back)
+  // is needed at the record; PTGS_GS_OV_FENCE=1 restores it: A/B switch)
+  static const unsigned ev_flags = [] {
+    const char* v = getenv("PTGS_GS_OV_FENCE");
+    return (unsigned)(hipEventDisableTiming | (v && !strcmp(v, "1") ? 0u : (unsigned)hipEventDisableSystemFence));
+  }();
+  for (hipEvent_t* ev : {&c->ov_call[0], &c->ov_call[1], &c->ov_call[2], &c->ov_done})
+    if (!*ev) HIPCHK(c, hipEventCreateWithFlags(ev, ev_flags));
+  // the next ring slot; the workspace there was last used depth calls ago, and the caller's stream at the
+  // start of the call after that one (depth - 1 calls ago) had finished it, blend included
+  const uint32_t cur = (c->ov_pos + 1) % depth;
+  c->ov_pos = cur;
+  c->splat = c->ov_ring[cur];
+  HIPCHK(c, hipEventRecord(c->ov_call[cur], s));
+  ov->fe = c->ov_stream;
+  ov->wait = c->ov_started >= depth - 1 ? c->ov_call[(cur + 1) % depth] : c->ov_call[cur];
+  ov->done = c->ov_done;
+  // the blend's tile order: the front end's order workgroup from the workspace's previous frame (default),
+  // or PTGS_GS_OV_ORDER=own: a launch behind the front end from the frame's own counts (A/B switch;
+  // measured slower at C2 static, 0.0531 vs 0.0521 ms, and not faster on the orbit: DESIGN §5 round 6)
+  static const bool own_order = [] {
+    const char* v = getenv("PTGS_GS_OV_ORDER");
+    return v && !strcmp(v, "own");
+  }();
+  ov->own_order = own_order;
+  c->ov_started = std::min(c->ov_started + 1u, (uint32_t)PTGS_OV_RING);
+  return PTGS_OK;
+}
+
 static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
                         const float bg[3], const float* depth, const float* under, uint32_t tile_row_begin,
                         uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream) {
   uint32_t report = 0;
+  SplatOverlap ov{};
+  const SplatOverlap* ovp = nullptr;
+  if (c->flags & PTGS_FLAG_SPLAT_OVERLAP) {
+    const int rc = splat_overlap_begin(c, (hipStream_t)stream, &ov);
+    if (rc != PTGS_OK) return rc;
+    ovp = &ov;  // (splat_gaussians runs a frame with stats / publish / stage timing serially anyway)
+  } else {
+    c->ov_started = 0;
+  }
   const int rc = splat_render(c, g, ubo, w, h, bg, depth, under, tile_row_begin, tile_row_end, out, stats, stream,
-                              &report);
+                              &report, ovp);
   return rc != PTGS_OK ? rc : splat_report(c, report);
 }
 
@@ -727,6 +832,7 @@ int ptgs_splat_gaussians_views(ptgs_ctx* c, const ptgs_gaussians* g, uint32_t n_
     if (!outs[v]) return fail(c, PTGS_EINVAL, "null output of view %u", v);
   if (n_views == 1) return splat_common(c, g, &ubos[0], w, h, bg, nullptr, nullptr, 0, ~0u, outs[0], nullptr, stream);
   HIPCHK(c, hipSetDevice(c->device));
+  c->ov_started = 0;  // (view 0 renders serially on the caller's stream with the latest workspace)
   const hipStream_t s = (hipStream_t)stream;
   if (!c->view_fork) HIPCHK(c, hipEventCreateWithFlags(&c->view_fork, hipEventDisableTiming));
   // every view's pair buffer starts from the largest pair count any slot has seen (views of one
@@ -805,22 +911,26 @@ int ptgs_splat_status_read(ptgs_ctx* c, ptgs_splat_status* out, void* stream) {
   HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
   for (int v = 1; v < PTGS_MAX_VIEWS; ++v)
     if (c->view_stream[v]) HIPCHK(c, hipStreamSynchronize(c->view_stream[v]));
+  if (c->ov_stream) HIPCHK(c, hipStreamSynchronize(c->ov_stream));
   *out = ptgs_splat_status{};
   out->pair_capacity = 0xFFFFFFFFu;
-  for (int v = 0; v < PTGS_MAX_VIEWS; ++v) {
-    SplatWorkspace* ws = v == 0 ? c->splat : c->view_ws[v];
-    if (!ws) continue;
+  // (slot 0 also holds the other ring workspaces of PTGS_FLAG_SPLAT_OVERLAP: indices >= PTGS_MAX_VIEWS here)
+  for (int v = 0; v < PTGS_MAX_VIEWS + PTGS_OV_RING; ++v) {
+    SplatWorkspace* ws = v == 0 ? c->splat : v < PTGS_MAX_VIEWS ? c->view_ws[v] : c->ov_ring[v - PTGS_MAX_VIEWS];
+    if (!ws || (v >= PTGS_MAX_VIEWS && ws == c->splat)) continue;
+    const int slot = v >= PTGS_MAX_VIEWS ? 0 : v;
     SplatStatusOut so;
     HIPCHK(c, splat_status(ws, true, &so));
-    out->views[v] = so.incomplete;
+    out->views[slot] += so.incomplete;
     out->frames += so.incomplete;
     out->spilled_tiles += so.spilled_tiles;
     out->incomplete_tiles += so.incomplete_tiles;
-    out->pair_capacity = std::min(out->pair_capacity, so.capacity);
-    out->last_pairs = std::max(out->last_pairs, so.last_pairs);
-    if (v == 0) {
-      out->spill_capacity = so.spill_capacity;
-      out->spill_demand = so.spill_demand;
+    if (v < PTGS_MAX_VIEWS || so.last_pairs) out->pair_capacity = std::min(out->pair_capacity, so.capacity);
+    // the latest frame's pairs: the current workspace's (slot 0), else any view's
+    if (v < PTGS_MAX_VIEWS) out->last_pairs = std::max(out->last_pairs, so.last_pairs);
+    if (slot == 0) {
+      out->spill_capacity = v == 0 ? so.spill_capacity : std::min(out->spill_capacity, so.spill_capacity);
+      out->spill_demand = std::max(out->spill_demand, so.spill_demand);
     }
   }
   if (c->splat) splat_front_end_info(c->splat, &out->touched_runs, &out->fused);
@@ -833,6 +943,8 @@ int ptgs_splat_reserve(ptgs_ctx* c, uint32_t pairs) {
   HIPCHK(c, splat_reserve(c->splat, pairs));
   for (int v = 1; v < PTGS_MAX_VIEWS; ++v)
     if (c->view_ws[v]) HIPCHK(c, splat_reserve(c->view_ws[v], pairs));
+  for (SplatWorkspace* w : c->ov_ring)
+    if (w && w != c->splat) HIPCHK(c, splat_reserve(w, pairs));
   return PTGS_OK;
 }
 

@@ -12,13 +12,25 @@ struct SplatWorkspace;
 SplatWorkspace* splat_workspace_create();
 void splat_workspace_destroy(SplatWorkspace* w);
 
+// Front end on a second stream (PTGS_FLAG_SPLAT_OVERLAP, fused frames): the front end (and, with
+// own_order, the blend's tile order from this frame's own pair counts) runs on `fe` once `wait` has
+// completed; `done` is recorded behind it and the caller's stream waits for it before the blend. So the
+// front end of frame k overlaps the blend of frame k - 1 (another workspace) on the caller's stream.
+struct SplatOverlap {
+  hipStream_t fe;
+  hipEvent_t wait, done;
+  bool own_order;
+};
+
 // view/mvp column-major float[16]; p00 = proj[0][0], p11 = proj[1][1] (negative: Vulkan y-down)
 // depth / under (both null, or both device arrays of W*H): the hybrid "over" composite
+// ov: null, or the front-end stream of an overlapped frame (see SplatOverlap; ignored by three-launch frames)
 hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const float* view, const float* mvp, float p00,
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
                            ptgs_splat_stats* stats, bool time_stages, bool publish, bool publish_tight, hipStream_t s,
-                           uint32_t* report);  // report: bit 0 an earlier frame was left incomplete, bit 1 ids >= N
+                           uint32_t* report,  // report: bit 0 an earlier frame was left incomplete, bit 1 ids >= N
+                           const SplatOverlap* ov = nullptr);
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
 // 3D Morton order of the means: a reordered copy + the original indices (synchronises s)
 hipError_t splat_sort_spatial(const ptgs_gaussians* g, float* means, float* scales, float* rots, float* opac,

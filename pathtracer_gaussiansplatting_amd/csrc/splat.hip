@@ -624,11 +624,17 @@ __device__ __forceinline__ void gs_walk_chunk(const BinGrid& bg, const ushort4* 
 #define GS_ORDER_B 4u  // previous tile counts in flight per work-item (16: 104 VGPRs in the front-end kernels)
 // (order[b] = the tile. Carrying the previous frame's count of the tile in the word, so the blend loads
 // only that much of the key row with the tile, measured slower: C2 0.0594 vs 0.0588 ms)
-__device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) {
-  const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
+__device__ __forceinline__ uint32_t gs_order_bucket_n(uint32_t n) {
   return GS_ORDER_BUCKETS - 1u - min(GS_ORDER_BUCKETS - 1u, n >> 1);
 }
-__device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restrict__ order, uint32_t tb, uint32_t te,
+__device__ __forceinline__ uint32_t gs_order_bucket(uint2 r) { return gs_order_bucket_n(r.y > r.x ? r.y - r.x : 0u); }
+// (COUNTS: prev holds one u32 pair count per tile, the fused front end's cursors of the frame itself)
+template <bool COUNTS = false>
+__device__ __forceinline__ uint32_t gs_order_bucket_at(const void* prev, uint32_t t) {
+  return COUNTS ? gs_order_bucket_n(static_cast<const uint32_t*>(prev)[t]) : gs_order_bucket(static_cast<const uint2*>(prev)[t]);
+}
+template <bool COUNTS = false>
+__device__ void gs_tile_order(const void* __restrict__ prev, uint32_t* __restrict__ order, uint32_t tb, uint32_t te,
                               uint32_t* s_h /* >= GS_ORDER_BUCKETS */) {
   // (the previous counts are loaded GS_ORDER_B per work-item at a time, all in flight before the first
   // is used: a loop of one load and one LDS atomic per iteration waited for every load, 16 dependent
@@ -641,7 +647,7 @@ __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restri
 #pragma unroll
     for (uint32_t j = 0; j < GS_ORDER_B; ++j) {
       const uint32_t t = t0 + j * nth;
-      bk[j] = t < te ? gs_order_bucket(prev[t]) : GS_ORDER_BUCKETS;
+      bk[j] = t < te ? gs_order_bucket_at<COUNTS>(prev, t) : GS_ORDER_BUCKETS;
     }
 #pragma unroll
     for (uint32_t j = 0; j < GS_ORDER_B; ++j)
@@ -663,12 +669,73 @@ __device__ void gs_tile_order(const uint2* __restrict__ prev, uint32_t* __restri
 #pragma unroll
     for (uint32_t j = 0; j < GS_ORDER_B; ++j) {
       const uint32_t t = t0 + j * nth;
-      bk[j] = t < te ? gs_order_bucket(prev[t]) : GS_ORDER_BUCKETS;
+      bk[j] = t < te ? gs_order_bucket_at<COUNTS>(prev, t) : GS_ORDER_BUCKETS;
     }
 #pragma unroll
     for (uint32_t j = 0; j < GS_ORDER_B; ++j)
       if (bk[j] < GS_ORDER_BUCKETS) order[atomicAdd(s_h + bk[j], 1u)] = t0 + j * nth;
   }
+}
+
+// The tile order of an overlapped fused frame (SplatOverlap::own_order), from the frame's OWN pair counts
+// (the cursors its front end has just reserved): it runs on the front-end stream behind the front end,
+// off the caller's stream, where the blend of the previous frame hides it; the in-kernel order
+// workgroup of a serial frame can only use the previous frame's counts.
+// Up to GS_ORDER_R * GS_ORDER_THREADS tiles (1080p: 8 160) each work-item keeps its tiles' buckets in
+// registers (one load round) and the histogram has GS_ORDER_COLS columns per bucket, one per lane & 15:
+// the LDS atomics of a wave's lanes on one bucket (most light tiles share a few buckets) meet 4-way
+// instead of 64-way (a single-column histogram serialised ~8k same-address atomics per pass, ~3.5 us).
+// Larger grids (4K) take the generic two-pass order.
+#ifndef GS_ORDER_THREADS
+#define GS_ORDER_THREADS 1024
+#endif
+#define GS_ORDER_COLS 16u
+#define GS_ORDER_R ((8192u + GS_ORDER_THREADS - 1u) / GS_ORDER_THREADS)
+#define GS_ORDER_E (GS_ORDER_BUCKETS * GS_ORDER_COLS / GS_ORDER_THREADS)  // scanned entries per work-item
+static_assert(GS_ORDER_E * GS_ORDER_THREADS == GS_ORDER_BUCKETS * GS_ORDER_COLS, "the order scan's split");
+__global__ __launch_bounds__(GS_ORDER_THREADS) void gs_tile_order_kernel(const uint32_t* __restrict__ counts,
+                                                                         uint32_t* __restrict__ order, uint32_t tb,
+                                                                         uint32_t te) {
+  __shared__ uint32_t s_h[GS_ORDER_BUCKETS * GS_ORDER_COLS];
+  __shared__ uint32_t s_part[GS_ORDER_THREADS / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, col = lane & (GS_ORDER_COLS - 1u);
+  if (te - tb > GS_ORDER_R * GS_ORDER_THREADS) {
+    gs_tile_order<true>(counts, order, tb, te, s_h);
+    return;
+  }
+  uint32_t bk[GS_ORDER_R];
+#pragma unroll
+  for (uint32_t j = 0; j < GS_ORDER_R; ++j) {
+    const uint32_t t = tb + tid + j * GS_ORDER_THREADS;
+    bk[j] = t < te ? gs_order_bucket_n(counts[t]) : GS_ORDER_BUCKETS;
+  }
+  for (uint32_t k = tid; k < GS_ORDER_BUCKETS * GS_ORDER_COLS; k += GS_ORDER_THREADS) s_h[k] = 0;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < GS_ORDER_R; ++j)
+    if (bk[j] < GS_ORDER_BUCKETS) atomicAdd(s_h + bk[j] * GS_ORDER_COLS + col, 1u);
+  __syncthreads();
+  // exclusive scan of the (bucket, column) counts in bucket-major order
+  uint32_t v[GS_ORDER_E], sum = 0;
+#pragma unroll
+  for (uint32_t e = 0; e < GS_ORDER_E; ++e) {
+    v[e] = s_h[tid * GS_ORDER_E + e];
+    sum += v[e];
+  }
+  const uint32_t incl = wave_incl_scan(sum);
+  if (lane == 63u) s_part[wave] = incl;
+  __syncthreads();
+  uint32_t ex = incl - sum;
+  for (uint32_t w = 0; w < wave; ++w) ex += s_part[w];
+#pragma unroll
+  for (uint32_t e = 0; e < GS_ORDER_E; ++e) {
+    s_h[tid * GS_ORDER_E + e] = ex;
+    ex += v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < GS_ORDER_R; ++j)
+    if (bk[j] < GS_ORDER_BUCKETS) order[atomicAdd(s_h + bk[j] * GS_ORDER_COLS + col, 1u)] = tb + tid + j * GS_ORDER_THREADS;
 }
 
 // Spill accounting (see gs_spill_tile), run by the first front-end launch's block (0, 0): the previous
@@ -1015,14 +1082,29 @@ struct GsFused {  // the sort's and the blend's view of a fused-front-end frame 
   uint2* fsq;             // the front end's slice queue (re-armed by block (0, 0): entries and fz[12..14])
   uint32_t fsq_cap;
 };
-#ifndef GS_FUSED_WG
-#define GS_FUSED_WG 512  // work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs)
+// Work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs): 512 for a frame on the
+// caller's stream; 256 for an overlapped frame (SplatOverlap), whose front end runs beside the previous
+// frame's blend: a 256-work-item workgroup of at most 64 VGPRs and ~14 KB of LDS takes the slot of one
+// retiring blend workgroup (256 work-items, 64 VGPRs, 17 KB), where a 512-work-item one waited for the
+// blend's tail (measured: the whole front end ran after the blend; C2 frames 63 vs 56 us serial).
+#define GS_FUSED_WG 512
+#ifndef GS_FUSED_WG_OV
+#define GS_FUSED_WG_OV 256
 #endif
+template <uint32_t WG> struct GsFusedShape;
+template <> struct GsFusedShape<512> {
+  static constexpr uint32_t slice = 4096u;  // pairs per slice (C2's chunks hold 1.6k on average, 3.3k at most: one slice)
+  static constexpr uint32_t lds_cap = 0u;   // histogram window in tiles (0: the band's)
+};
+template <> struct GsFusedShape<256> {
+  static constexpr uint32_t slice = 2048u;
+  static constexpr uint32_t lds_cap = 2048u;  // 8 KB (+ 5.6 KB static): within one blend workgroup's LDS
+};
 
 // The count walk of one slice [p0, p1) of a chunk's pairs (at most GS_FUSED_QREG per work-item): the
 // chunk's rects (s_e: x0 | w << 16, y0 | h << 16, key index, depth bits) and the inclusive scan of
 // their areas (s_incl) are in LDS; work-item t takes the contiguous pairs [p0 + t q, p0 + t q + q)
-// (q = ceil((p1 - p0) / GS_FUSED_WG)): one binary search for its first pair, then it steps through the
+// (q = ceil((p1 - p0) / WG)): one binary search for its first pair, then it steps through the
 // rects (a heavy Gaussian's pairs are spread over the whole workgroup instead of one wave). Returning
 // LDS atomics give each pair its rank among the slice's pairs of its tile, kept in registers with the
 // pair, packed as k | rank << 13 | j << 21 (k: tile in the chunk's rect, < 8192 = GS_BAND_TILES; rank
@@ -1030,14 +1112,17 @@ struct GsFused {  // the sort's and the blend's view of a fused-front-end frame 
 // kept pair at its run's base + rank without walking the rects again or touching an LDS atomic.
 // Returns the work-item's pair count.
 #ifndef GS_FUSED_QREG
-#define GS_FUSED_QREG 8  // pairs per work-item of a slice (GS_FUSED_SLICE / GS_FUSED_WG; C2 needs <= 7)
+#define GS_FUSED_QREG 8  // pairs per work-item of a slice (GsFusedShape<WG>::slice / WG; C2 needs <= 7)
 #endif
 #define GS_KEEP_RB (GS_FUSED_THREADS <= 256 ? 8u : 9u)  // bits of rank and of j (< GS_FUSED_THREADS)
 static_assert(GS_FUSED_THREADS <= 512 && GS_BAND_TILES <= 8192, "gs_wg_count_keep's packing");
+#define GS_PK_NONE 0xFFFFFFFFu  // a walked pair outside the histogram window (kept by another window's walk)
+template <uint32_t WG>
 __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, const uint4* s_e, uint32_t ng, uint32_t p0,
                                                      uint32_t p1, uint32_t* s_hist, uint32_t bx0, uint32_t by0,
-                                                     uint32_t rw, uint32_t (&pk)[GS_FUSED_QREG]) {
-  const uint32_t q = (p1 - p0 + GS_FUSED_WG - 1) / GS_FUSED_WG;
+                                                     uint32_t rw, uint32_t kw, uint32_t kcap,
+                                                     uint32_t (&pk)[GS_FUSED_QREG]) {
+  const uint32_t q = (p1 - p0 + WG - 1) / WG;
   uint32_t p = p0 + threadIdx.x * q;
   const uint32_t pe = min(p1, p + q);
   if (p >= pe) return 0;
@@ -1055,9 +1140,14 @@ __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, con
 #pragma unroll
   for (uint32_t c = 0; c < GS_FUSED_QREG; ++c) {
     if (c < cnt) {
-      const uint32_t k = ((e.y & 0xFFFFu) + ry - by0) * rw + ((e.x & 0xFFFFu) + rx - bx0);
-      const uint32_t rank = atomicAdd(s_hist + k, 1u);
-      pk[c] = k | (rank << 13) | (j << (13u + GS_KEEP_RB));
+      // (the tile's index in the rect, relative to the histogram window [kw, kw + kcap))
+      const uint32_t k = ((e.y & 0xFFFFu) + ry - by0) * rw + ((e.x & 0xFFFFu) + rx - bx0) - kw;
+      if (k < kcap) {
+        const uint32_t rank = atomicAdd(s_hist + k, 1u);
+        pk[c] = k | (rank << 13) | (j << (13u + GS_KEEP_RB));
+      } else {
+        pk[c] = GS_PK_NONE;
+      }
       if (c + 1 < cnt && ++rx == w) {
         rx = 0;
         if (++ry == (e.y >> 16)) {  // next rect with pairs
@@ -1073,7 +1163,7 @@ __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, con
   return cnt;
 }
 
-// Load balance. A chunk's pairs are walked in slices of at most GS_FUSED_SLICE pairs. The owner (the
+// Load balance. A chunk's pairs are walked in slices of at most GsFusedShape<WG>::slice pairs. The owner (the
 // chunk's workgroup) walks slice 0 and publishes the others to a queue (fsq, entries (owner + 1, j));
 // helper workgroups (the rows after the owners) claim queued slices, rebuild the chunk's rects (the
 // same preprocess, no stores) and walk them: every (slice, tile) run reserves its own range, so a
@@ -1084,25 +1174,22 @@ __device__ __forceinline__ uint32_t gs_wg_count_keep(const uint32_t* s_incl, con
 // is then its owner's). Queue words: fz[GS_FSQ_W] claims (helpers), fz[GS_FSQ_W + 1] entries,
 // fz[GS_FSQ_W + 2] owners done;
 // entries are 0 (not written), owner + 1 (open), GS_FSQ_TAKEN; the blend's block (0, 0) re-arms them.
-#ifndef GS_FUSED_SLICE
-#define GS_FUSED_SLICE 4096u  // pairs per slice (C2's chunks hold 1.6k on average, 3.3k at most: one slice)
-#endif
 #ifndef GS_FUSED_HELPERS
 #define GS_FUSED_HELPERS 128u  // helper workgroups per band (one queued slice each)
 #endif
 #define GS_FSQ_TAKEN 0xFFFFFFFFu
 #define GS_FSQ_W 32  // the queue words' offset in fz: a cache line of their own (helpers poll them)
-#ifndef GS_FUSED_WAVES
-#define GS_FUSED_WAVES 6  // waves per SIMD (3 workgroups of 512 work-items per CU; 8 forces SGPR spills)
-#endif
-static_assert(GS_FUSED_SLICE <= (uint32_t)GS_FUSED_WG * GS_FUSED_QREG, "a slice's pairs are kept in registers");
+// waves per SIMD: 512 work-items 6 (3 workgroups per CU; 8 forced SGPR spills), 256 work-items 8 (64 VGPRs)
+#define GS_FUSED_WAVES(WG) ((WG) == 512 ? 6 : 8)
+static_assert(GsFusedShape<512>::slice <= 512u * GS_FUSED_QREG && GsFusedShape<256>::slice <= 256u * GS_FUSED_QREG,
+              "a slice's pairs are kept in registers");
 // chunk skip flags (cskip) and chunk bounds are per 256 Gaussians (ptgs_gaussians_chunk_bounds): the fused
 // workgroups index them by their own chunk, so a fused chunk must be exactly that
 static_assert(GS_FUSED_THREADS == 256, "the fused chunk is the chunk-bounds granule (256 Gaussians)");
 
 
-template <bool ROWCULL>
-__global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
+template <bool ROWCULL, uint32_t WG>
+__global__ __launch_bounds__(WG, GS_FUSED_WAVES(WG)) void gs_bin_fused_kernel(SplatCam cam, PreArgs A, BinGrid bg,
                                                                          uint32_t scap,
                                                                          uint32_t* __restrict__ cursor,
                                                                          uint32_t* __restrict__ fz,
@@ -1115,10 +1202,13 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
                                                                          ushort4* __restrict__ rects_out,
                                                                          float* __restrict__ depths_out,
                                                                          uint32_t* k_host, uint2* __restrict__ fsq,
-                                                                         uint32_t fsq_cap) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // <= band_rows * grid_x
-  __shared__ uint32_t s_red[4][GS_FUSED_WG / 64];
-  __shared__ uint32_t s_tot[GS_FUSED_WG / 64];
+                                                                         uint32_t fsq_cap, uint32_t kcap) {
+  // the histogram window: kcap entries (<= band_rows * grid_x); a chunk whose bounding tile rect holds
+  // more tiles walks its slice once per window of kcap tiles (each walk counts, reserves and scatters
+  // only its window's pairs), so the dynamic LDS need not cover a whole band
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+  __shared__ uint32_t s_red[4][WG / 64];
+  __shared__ uint32_t s_tot[WG / 64];
   __shared__ uint32_t s_incl[GS_FUSED_THREADS];
   __shared__ uint4 s_e[GS_FUSED_THREADS];
   __shared__ uint32_t s_job[4];  // helpers: (owner, slice) claimed; owners: queue base of their slices
@@ -1250,7 +1340,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
     STAMP(0, 7);
     uint32_t run = incl, P = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < GS_FUSED_WG / 64; ++w) {
+    for (uint32_t w = 0; w < WG / 64; ++w) {
       bx0 = min(bx0, s_red[0][w]);
       by0 = min(by0, s_red[1][w]);
       bx1 = max(bx1, s_red[2][w]);
@@ -1267,7 +1357,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
     by1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)by1);
     P = (uint32_t)__builtin_amdgcn_readfirstlane((int)P);
     const uint32_t rw = bx1 > bx0 ? bx1 - bx0 : 0u, rh = by1 > by0 ? by1 - by0 : 0u, nt = rw * rh;
-    const uint32_t nsl = (P + GS_FUSED_SLICE - 1u) / GS_FUSED_SLICE;  // slices of this chunk (uniform)
+    const uint32_t nsl = (P + GsFusedShape<WG>::slice - 1u) / GsFusedShape<WG>::slice;  // slices of this chunk (uniform)
     if (owner) {
       if (threadIdx.x == 0) {  // the workgroup's bounding rect (gs_spill_tile; empty: x0 > x1)
         crect[wg] = nt ? make_ushort4((unsigned short)bx0, (unsigned short)by0, (unsigned short)bx1, (unsigned short)by1)
@@ -1297,25 +1387,29 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
     // the slices this pass walks: helpers one; owners slice 0, then each queued slice it can still
     // claim (or every slice when the queue was full)
     for (;;) {
-      const uint32_t p0 = slice * GS_FUSED_SLICE, p1 = min(P, p0 + GS_FUSED_SLICE);
-      for (uint32_t k = threadIdx.x; k < nt; k += GS_FUSED_WG) s_hist[k] = 0;
+      const uint32_t p0 = slice * GsFusedShape<WG>::slice, p1 = min(P, p0 + GsFusedShape<WG>::slice);
+     for (uint32_t kw = 0; kw < nt; kw += kcap) {  // histogram windows of the rect (one for most chunks)
+      const uint32_t nw = min(kcap, nt - kw);
+      if (kw) __syncthreads();  // (the previous window's scatter has read s_hist)
+      for (uint32_t k = threadIdx.x; k < nw; k += WG) s_hist[k] = 0;
       __syncthreads();  // (the scan and the zeroed histogram)
       STAMP(0, 1);
       STAMP_SYNC();
       STAMP(0, 2);
       uint32_t pk[GS_FUSED_QREG];
-      const uint32_t kept = p1 > p0 ? gs_wg_count_keep(s_incl, s_e, GS_FUSED_THREADS, p0, p1, s_hist, bx0, by0, rw, pk) : 0u;
+      const uint32_t kept =
+          p1 > p0 ? gs_wg_count_keep<WG>(s_incl, s_e, GS_FUSED_THREADS, p0, p1, s_hist, bx0, by0, rw, kw, kcap, pk) : 0u;
       __syncthreads();
       STAMP(0, 3);
       // reserve: one returning atomic per touched tile (all of a work-item's issued before any is
       // used); the LDS entry becomes the run's base
       const float rcp_rw = 1.0f / (float)max(rw, 1u);
-      for (uint32_t k0 = threadIdx.x; k0 < nt; k0 += 4 * GS_FUSED_WG) {
+      for (uint32_t k0 = threadIdx.x; k0 < nw; k0 += 4 * WG) {
         uint32_t c[4], t[4], base[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint32_t k = k0 + j * GS_FUSED_WG;
-          c[j] = k < nt ? s_hist[k] : 0u;
+          const uint32_t kl = k0 + j * WG, k = kw + kl;
+          c[j] = kl < nw ? s_hist[kl] : 0u;
           uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13 * 2^13: exact after the fix-ups
           ry = ry * rw > k ? ry - 1 : ry;
           ry = (ry + 1) * rw <= k ? ry + 1 : ry;
@@ -1326,7 +1420,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (!c[j]) continue;
-          s_hist[k0 + j * GS_FUSED_WG] = base[j];
+          s_hist[k0 + j * WG] = base[j];
           acc_pairs += c[j];
           ++acc_res;
           if (base[j] <= scap && base[j] + c[j] > scap) atomicAdd(fz + 5, 1u);  // (one crossing per spilled tile)
@@ -1340,8 +1434,9 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
       STAMP(0, 4);
 #pragma unroll
       for (uint32_t c = 0; c < GS_FUSED_QREG; ++c) {
-        if (c < kept) {
-          const uint32_t k = pk[c] & 0x1FFFu, rel = s_hist[k] + ((pk[c] >> 13) & ((1u << GS_KEEP_RB) - 1u));
+        if (c < kept && pk[c] != GS_PK_NONE) {
+          const uint32_t kl = pk[c] & 0x1FFFu, k = kw + kl;
+          const uint32_t rel = s_hist[kl] + ((pk[c] >> 13) & ((1u << GS_KEEP_RB) - 1u));
           const uint4 e = s_e[pk[c] >> (13u + GS_KEEP_RB)];
           uint32_t ry = (uint32_t)((float)k * rcp_rw);  // k < 2^13: exact after the fix-ups
           ry = ry * rw > k ? ry - 1 : ry;
@@ -1353,6 +1448,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
           }
         }
       }
+     }  // (windows)
       if (!owner) break;
       // owner: the next of its slices that no helper has taken (uniform through LDS)
       __syncthreads();  // (every read of s_hist / s_job before they change)
@@ -1387,7 +1483,7 @@ __global__ __launch_bounds__(GS_FUSED_WG, GS_FUSED_WAVES) void gs_bin_fused_kern
   __syncthreads();
   if (threadIdx.x == 0) {  // per-workgroup partials (the blend's block (0, 0) sums them: no fan-in atomics)
     uint32_t p = 0, r = 0;
-    for (uint32_t w = 0; w < GS_FUSED_WG / 64; ++w) {
+    for (uint32_t w = 0; w < WG / 64; ++w) {
       p += s_red[0][w];
       r += s_red[1][w];
     }
@@ -1891,6 +1987,9 @@ __device__ const uint32_t* gs_spill_tile(const GsSpill& sp, uint32_t tx, uint32_
 // chain, the termination applied without its wave-uniform branch, an XCD-aware tile mapping, loading the
 // key row only up to the previous frame's count, non-temporal records / key rows.
 #define GS_DONE_EVERY 4u  // list entries between the wave's all-pixels-done tests (a power of two >= 4)
+// (Measured and rejected, round 6: the quadratic as three packed v_pk_mul / v_pk_fma_f32 over the record's
+// (A, C) (B, D) (E, F) pairs plus one add, and red / green as one packed FMA: 13 VALU per entry instead of
+// 15, but C2 0.0574 vs 0.0558 ms: the packed ops' dependency stalls (s_nop) lengthen each wave's chain.)
 #ifndef GS_BLEND_MIN_BLOCKS
 #define GS_BLEND_MIN_BLOCKS 8  // 64 VGPRs: 8 waves per SIMD (vs 7 at 70 VGPRs): +3% at C2
 #endif
@@ -2084,7 +2183,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     uint32_t r = lane;
     if (wave < m) r += gs_runs_below<GS_BLOCK / 64>(s_key, m, wave, sk);
     __syncthreads();  // every read of the keys is done before records overwrite them
-    if (tid < n) s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, true);
+    if (tid < n) s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, !GS_PROBE(GS_PROBE_NO_EXACT));
     if (sk != ~0ull) {
       if (pub) {
         keys_out[range.x + r] = tbits | (sk >> 32);
@@ -2113,7 +2212,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     }
     __syncthreads();  // every read of the keys is done before records overwrite them
     if (tid < n) {
-      s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, true);
+      s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, !GS_PROBE(GS_PROBE_NO_EXACT));
       if (pub) {
         keys_out[range.x + r] = tbits | (key >> 32);
         vals_out[range.x + r] = (uint32_t)(key >> 8) & 0xFFFFFFu;
@@ -2347,9 +2446,10 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
                            ptgs_splat_stats* stats, bool time_stages, bool publish, bool publish_tight, hipStream_t s,
-                           uint32_t* report) {
+                           uint32_t* report, const SplatOverlap* ov) {
   hipError_t e;
   *report = 0;
+  if (stats || publish || time_stages) ov = nullptr;  // (these frames are synchronous or instrumented: serial)
   if (time_stages && !w->ev[0])
     for (hipEvent_t& ev : w->ev)
       if ((e = hipEventCreate(&ev))) return e;
@@ -2529,10 +2629,10 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = ensure(w->cskip, nch))) return e;
     pa.cskip = (const uint8_t*)w->cskip.p;
   }
-  auto cull_flags = [&]() -> hipError_t {
+  auto cull_flags = [&](hipStream_t cs) -> hipError_t {
     if (!cam.cull) return hipSuccess;
     const uint32_t nch = (n + 255u) / 256u;
-    hipLaunchKernelGGL(gs_chunk_cull_kernel, dim3((nch + 255u) / 256u), dim3(256), 0, s, cam,
+    hipLaunchKernelGGL(gs_chunk_cull_kernel, dim3((nch + 255u) / 256u), dim3(256), 0, cs, cam,
                        (const float4*)g->chunk_bounds, nch, (uint8_t*)w->cskip.p);
     return hipGetLastError();
   };
@@ -2627,9 +2727,12 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e2 = ensure(w->tile_slots, (size_t)tiles * scap * 8))) return e2;
     if ((e2 = ensure(w->vals_out, (size_t)tiles * scap * 4))) return e2;
     if (publish && (e2 = ensure(w->keys_out, (size_t)tiles * scap * 8))) return e2;
+    // the front end's stream: the caller's, or (overlapped frame) the second stream once ov->wait is done
+    const hipStream_t sf = ov ? ov->fe : s;
+    if (ov && (e2 = hipStreamWaitEvent(sf, ov->wait, 0))) return e2;
     if (w->cursor.bytes < (size_t)tiles * 4) {  // zero between frames (the blend re-arms what it reads)
       if ((e2 = ensure(w->cursor, (size_t)tiles * 4))) return e2;
-      if ((e2 = hipMemsetAsync(w->cursor.p, 0, w->cursor.bytes, s))) return e2;
+      if ((e2 = hipMemsetAsync(w->cursor.p, 0, w->cursor.bytes, sf))) return e2;
     }
     // helper workgroups only when the latest fused frame queued slices (k_host[11]: a static view whose
     // chunks all fit one slice launches none; the owners walk any slice no helper takes, so a frame
@@ -2647,17 +2750,17 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e2 = ensure(w->fzp, (size_t)nwg * 8))) return e2;
     // slice queue: room for twice the slices of the largest pair count seen (+ one per owner); zero
     // once here, re-armed by the blend after every frame
-    const uint32_t qcap = std::max<uint32_t>(4096u, 2u * (w->k_host[0] / GS_FUSED_SLICE) + nwg_fused);
+    const uint32_t qcap = std::max<uint32_t>(4096u, 2u * (w->k_host[0] / GsFusedShape<256>::slice) + nwg_fused);
     if (w->fsq.bytes < (size_t)qcap * 8) {
       if ((e2 = ensure(w->fsq, (size_t)qcap * 8))) return e2;
-      if ((e2 = hipMemsetAsync(w->fsq.p, 0, w->fsq.bytes, s))) return e2;
+      if ((e2 = hipMemsetAsync(w->fsq.p, 0, w->fsq.bytes, sf))) return e2;
     }
     const uint32_t fsq_cap = (uint32_t)std::min<size_t>(w->fsq.bytes / 8, 0x7FFFFFFFu);
     GsFused fu = {scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
                   (uint32_t*)w->fzp.p, nwg, order, (uint2*)w->fsq.p, fsq_cap};
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers (band 0 stores them for gs_spill_tile)
     if (cam.cull && (n + 255u) / 256u > GS_FUSED_OWN_CULL) {
-      if ((e2 = cull_flags())) return e2;
+      if ((e2 = cull_flags(sf))) return e2;
       fpa.cbounds = nullptr;
     }
     fpa.rects = nullptr;
@@ -2665,14 +2768,34 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     BinGrid fg = bgrid;
     fg.chunks = (n + GS_FUSED_THREADS - 1) / GS_FUSED_THREADS;
     fg.chunk = GS_FUSED_THREADS;
-    hipLaunchKernelGGL(cam.rowcull ? gs_bin_fused_kernel<true> : gs_bin_fused_kernel<false>,
-                       dim3(fg.bands, fg.chunks + helpers + (order ? 1u : 0u)),
-                       dim3(GS_FUSED_WG), band_lds, s,
+    // the tile order: the front end's extra workgroup from the previous frame's counts, or (overlapped,
+    // own_order) a launch behind the front end from this frame's own counts
+    const bool own_order = order && ov && ov->own_order;
+    uint32_t* fe_order = own_order ? nullptr : order;
+    // the workgroup shape (GsFusedShape: 256 work-items beside another frame's blend, else 512; PTGS_GS_FE_WG
+    // overrides: A/B switch) and its histogram window (entries; 0: the whole band; at least the order's buckets)
+    static const int wg_env = [] {
+      const char* v = getenv("PTGS_GS_FE_WG");
+      return v ? atoi(v) : 0;
+    }();
+    const uint32_t fwg = wg_env == 256 || wg_env == 512 ? (uint32_t)wg_env : ov ? (uint32_t)GS_FUSED_WG_OV : (uint32_t)GS_FUSED_WG;
+    const uint32_t cap = fwg == 256 ? GsFusedShape<256>::lds_cap : GsFusedShape<512>::lds_cap;
+    const size_t fe_lds = std::max<size_t>(cap ? std::min<size_t>(band_lds, (size_t)cap * 4u) : band_lds,
+                                           (size_t)GS_ORDER_BUCKETS * 4u);
+    auto fk = fwg == 256 ? (cam.rowcull ? gs_bin_fused_kernel<true, 256> : gs_bin_fused_kernel<false, 256>)
+                         : (cam.rowcull ? gs_bin_fused_kernel<true, 512> : gs_bin_fused_kernel<false, 512>);
+    hipLaunchKernelGGL(fk, dim3(fg.bands, fg.chunks + helpers + (fe_order ? 1u : 0u)), dim3(fwg), fe_lds, sf,
                        cam, fpa, fg, scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, (uint32_t*)w->fzp.p,
-                       (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, order,
+                       (unsigned long long*)w->tile_slots.p, (const uint2*)w->ranges.p, fe_order,
                        cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x, (ushort4*)w->crect.p, (ushort4*)w->rect.p,
-                       (float*)w->depths.p, w->k_dev, (uint2*)w->fsq.p, fsq_cap);
+                       (float*)w->depths.p, w->k_dev, (uint2*)w->fsq.p, fsq_cap, (uint32_t)(fe_lds / 4u));
     if ((e2 = hipGetLastError())) return e2;
+    if (own_order) {
+      hipLaunchKernelGGL(gs_tile_order_kernel, dim3(1), dim3(GS_ORDER_THREADS), 0, sf, (const uint32_t*)w->cursor.p,
+                         order, cam.row_begin * cam.grid_x, cam.row_end * cam.grid_x);
+      if ((e2 = hipGetLastError())) return e2;
+    }
+    if (ov && ((e2 = hipEventRecord(ov->done, sf)) || (e2 = hipStreamWaitEvent(s, ov->done, 0)))) return e2;
     if ((e2 = mark(1)) || (e2 = mark(2)) || (e2 = mark(3))) return e2;
     unsigned long long* keys_out = publish ? (unsigned long long*)w->keys_out.p : nullptr;
     const bool sort_large = w->k_host[1] > GS_MID;
@@ -2746,7 +2869,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
   auto enqueue_three = [&]() -> hipError_t {
     hipError_t e2;
     if ((e2 = ensure(w->tile_slots, (size_t)tiles * GS_TILE_SLOTS * 8))) return e2;
-    if ((e2 = cull_flags())) return e2;
+    if ((e2 = cull_flags(s))) return e2;
     // (n == 0: one chunk of nothing; the count still zeroes the histograms and the colscan publishes K = 0)
     hipLaunchKernelGGL(cam.rowcull ? gs_bin_count_kernel<true> : gs_bin_count_kernel<false>,
                        dim3(bgrid.bands, bgrid.chunks + (order ? 1u : 0u)), dim3(GS_COUNT_THREADS),

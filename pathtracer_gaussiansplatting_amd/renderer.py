@@ -216,6 +216,13 @@ class Renderer:
         self._publish = (self._publish & ~_abi.FLAG_PT_WAVEFRONT) | (_abi.FLAG_PT_WAVEFRONT if on else 0)
         self.set_flags(getattr(self, "_flags", 0))
 
+    def set_splat_overlap(self, on: bool):
+        """Frames in flight for splat_gaussians (PTGS_FLAG_SPLAT_OVERLAP): the front end of each
+        stream-ordered call runs on a second stream while the previous call's blend runs on the caller's.
+        The Gaussians must not be rewritten on the stream between two such calls (see ptgs.h)."""
+        self._publish = (self._publish & ~_abi.FLAG_SPLAT_OVERLAP) | (_abi.FLAG_SPLAT_OVERLAP if on else 0)
+        self.set_flags(getattr(self, "_flags", 0))
+
     def stats_reset(self, stream=None):
         self._chk(self.lib.ptgs_stats_reset(self._h, _stream(stream)), "ptgs_stats_reset")
 

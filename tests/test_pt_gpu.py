@@ -304,3 +304,17 @@ def test_ingested_scene_json(pt, oracle_lib):
     err, nd = _compare(g, o, sg, so)
     print(f"ingested scene rel L2 {err:.2e}, {nd} pixels differ")
     assert float(g[..., :3].mean()) > 1e-3
+
+
+def test_bvh_node_window_guard(pt, monkeypatch):
+    """the traversal addresses 4-wide nodes through a buffer descriptor with 32-bit offsets
+    (2 GiB, ~16.7M nodes). ptgs_scene_upload refuses a larger tree with PTGS_ERANGE instead of tracing
+    zero boxes; PTGS_BVH_NODE_LIMIT lowers the limit so a small scene exercises the refusal."""
+    from pathtracer_gaussiansplatting_amd._abi import PtgsError
+    sc = U.cornell()
+    monkeypatch.setenv("PTGS_BVH_NODE_LIMIT", "1")
+    with pytest.raises(PtgsError, match="PTGS_ERANGE"):
+        pt.upload_scene(sc)
+    monkeypatch.delenv("PTGS_BVH_NODE_LIMIT")
+    info = pt.upload_scene(sc)
+    assert info.num_bvh_nodes > 1
