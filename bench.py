@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-torus", action="store_true", help="skip the torus data-collection leg (SURVEY 8f #1)")
     ap.add_argument("--no-capture", action="store_true", help="skip the dataset capture / export leg (SURVEY 8f #4)")
     ap.add_argument("--no-gs-1m", action="store_true", help="skip the 1M-Gaussian splat and the point-cloud init legs")
+    ap.add_argument("--no-splat-overlap", action="store_true",
+                    help="time the C2 splat one frame at a time (default: frames in flight, PTGS_FLAG_SPLAT_OVERLAP)")
     ap.add_argument("--no-gs-10m", action="store_true", help="skip the 10M-Gaussian 3840x2160 splat leg (C5's splat)")
     ap.add_argument("--hybrid-gaussians", type=int, default=1_000_000)
     ap.add_argument("--hybrid-spp", type=int, default=16)
@@ -360,6 +362,12 @@ def main():
         from pathtracer_gaussiansplatting_amd import cornell_box_scene
         gubo = make_ubo(gpose, cornell_box_scene(), 0)
         img = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        # frames in flight (the viewer's loop; reference MAX_FRAMES_IN_FLIGHT = 2, engine.h:33): each call's
+        # front end runs on the context's second stream beside the previous calls' blends, which stay ordered
+        # on `stream` (PTGS_FLAG_SPLAT_OVERLAP; same images bit for bit, tests/test_splat_moving_gpu.py).
+        # Every frame still runs its own preprocess, binning, sort and blend.
+        gs_overlap = not args.no_splat_overlap
+        r.set_splat_overlap(gs_overlap)
         for _ in range(max(args.warmup, 1)):
             r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
         torch.cuda.synchronize()
@@ -411,6 +419,43 @@ def main():
         barrier()
         gdt = max_over_ranks(time.perf_counter() - t0)
         c2_spilled = assert_complete(r, "C2 timed loop")
+
+        def frame_latency_ms():  # one frame from its call to its image, alone (median of 21)
+            lat = []
+            for _ in range(21):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                gs_step()
+                torch.cuda.synchronize()
+                lat.append((time.perf_counter() - t1) * 1e3)
+            return float(np.median(lat))
+
+        gs_lat = frame_latency_ms()
+        gs_serial = None
+        if gs_overlap and not args.headline_only:  # the same loop one frame at a time (secondary figure)
+            r.set_splat_overlap(False)
+            tw = time.perf_counter()
+            while time.perf_counter() - tw < 0.2:
+                for _ in range(20):
+                    gs_step()
+                torch.cuda.synchronize()
+            r.splat_status(stream)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(gsteps):
+                gs_step()
+            if world > 1 and native_comm:
+                gs_pipe.wait()
+            torch.cuda.synchronize()
+            barrier()
+            sdt = max_over_ranks(time.perf_counter() - t0)
+            assert_complete(r, "C2 serial loop")
+            gs_serial = {"value": round(args.gaussians / (sdt / gsteps) / 1e9, 4),
+                         "unit": "Gsplats/s", "ms_per_step": round(sdt / gsteps * 1e3, 4),
+                         "frame_latency_ms": round(frame_latency_ms(), 4),
+                         "note": "one frame at a time on the caller's stream (front end, then blend)"}
+        r.set_splat_overlap(False)
         # the same frames from the Gaussians in their generated (random) order: the same image bit for
         # bit, timed alone (secondary figure)
         udt = None
@@ -456,6 +501,11 @@ def main():
         gms = gdt / gsteps * 1e3
         out["gs"] = {
             "value": round(N / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
+            "frames_in_flight": ("on: each call's front end on the context's second stream beside the previous calls' "
+                                 "blends (PTGS_FLAG_SPLAT_OVERLAP, 3 workspaces), every frame fully rendered")
+            if gs_overlap else "off",
+            "frame_latency_ms": round(gs_lat, 4),
+            "serial": gs_serial,
             "workload": f"C2 3DGS forward: {N} synthetic Gaussians, {W}x{H}", "pairs_K": int(K),
             "pairs_K_3sigma": K_exact,
             "skipped_frames": 0,  # incomplete frames: checked after every timed splat loop (ptgs_splat_status_read)
@@ -465,7 +515,14 @@ def main():
             + (" (ptgs_gather_rows, RCCL, on a second stream: frame f's gather overlaps frame f + 1's band)"
                if native_comm else " (gloo rehearsal, host copies)"),
             "front_end": "fused single launch" if gstat.fused else "count + colscan + scatter",
-            "stages_ms": {k: round(float(v), 4) for k, v in
+            # per-stage split: kernel-trace averages of this libptgs.so when profiled (profiles/traffic_latest.json),
+            # else per-stage HIP events of an untimed serial pass (each event pair adds its launch gap: the stages
+            # sum past ms_per_step, which is the timed frame)
+            "stages_us_kernel_trace": {k: round(float(e["avg_ms"]) * 1e3, 2) for k, e in
+                                       (("front_end_overlapped", _profiled("gs_bin_fused_kernel_ov")),
+                                        ("front_end_serial", _profiled("gs_bin_fused_kernel")),
+                                        ("sort_blend", _profiled("gs_sort_blend_kernel"))) if e} or None,
+            "stages_ms_event_timed": {k: round(float(v), 4) for k, v in
                           zip(["front_end" if gstat.fused else "preprocess+count", "colscan", "scatter", "sort_large",
                                "-", "sort_blend"], stages) if k != "-" and not (gstat.fused and k in ("colscan", "scatter"))},
             "gaussian_order": f"3D Morton order of the means (ptgs_gaussians_sort_spatial, {prep_ms:.2f} ms once, "
@@ -478,16 +535,20 @@ def main():
                          "frac": round(b_gs / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "alg_bytes": b_gs},
         }
         # per-kernel roofline of the blend (the dominant 3DGS kernel): counter-measured HBM bytes per launch
-        # over its HIP-event time (stage events, untimed pass); algorithmic bytes = 8-B key + 48-B record
-        # per pair read, 16 B per pixel written (no publish in production frames)
-        blend_ms = float(stages[5])
+        # over its kernel-trace duration (rocprofv3 of this libptgs.so, profiles/traffic_latest.json; the
+        # per-stage HIP events of the untimed serial pass when no matching profile exists: they inflate each
+        # stage by its event gaps); algorithmic bytes = 8-B key + 48-B record per pair read, 16 B per pixel
+        # written (no publish in production frames)
         bprof = _profiled("gs_sort_blend_kernel")
+        blend_ms = float(bprof["avg_ms"]) if bprof and bprof.get("avg_ms") else float(stages[5])
         b_alg = K * (8 + 48) + W * H * 16
         out["gs"]["roofline_blend"] = _roofline("gs_sort_blend_kernel", bprof["hbm_bytes_per_launch"] if bprof else None,
                                                 blend_ms, bprof, {
             "bound": "hbm", "achieved": round(b_alg / (blend_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(b_alg / (blend_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "alg_bytes_per_launch": b_alg,
+            "time_basis": "rocprofv3 kernel-trace average of this libptgs.so (profiles/traffic_latest.json)" if bprof
+                          else "per-stage HIP events (untimed serial pass)",
             "note": "algorithmic: 8-B key + 48-B blend record per (Gaussian, tile) pair + 16 B per pixel"})
         out["gs"]["splat_pairs_per_s"] = round(K / (gdt / gsteps) / 1e9, 4)  # (Gaussian, tile) instances, G/s
         if world == 1 and not args.headline_only:
@@ -516,16 +577,24 @@ def main():
             # stream-ordered (rows, pair buffer and tile order from the previous frame), timed in one run;
             # tiles that outgrow the buffers are completed through the spill pool (counted)
             orbit = gs_orbit_ubos(Camera, make_ubo, cornell_box_scene(), W, H, max(gsteps, 120))
-            for u in orbit[:3]:
-                r.splat_gaussians(dg, u, W, H, img, stream=stream)
-            torch.cuda.synchronize()
-            r.splat_status(stream)
-            t0 = time.perf_counter()
-            for u in orbit:
-                r.splat_gaussians(dg, u, W, H, img, stream=stream)
-            torch.cuda.synchronize()
-            odt = (time.perf_counter() - t0) / len(orbit)
+
+            def orbit_pass():
+                for u in orbit[:6]:
+                    r.splat_gaussians(dg, u, W, H, img, stream=stream)
+                torch.cuda.synchronize()
+                r.splat_status(stream)
+                t1 = time.perf_counter()
+                for u in orbit:
+                    r.splat_gaussians(dg, u, W, H, img, stream=stream)
+                torch.cuda.synchronize()
+                return (time.perf_counter() - t1) / len(orbit)
+
+            r.set_splat_overlap(gs_overlap)  # (frames in flight, as the C2 loop)
+            odt = orbit_pass()
             o_spilled = assert_complete(r, "gs_orbit")
+            r.set_splat_overlap(False)
+            odt_serial = orbit_pass() if gs_overlap else odt
+            assert_complete(r, "gs_orbit serial")
             # the timed frames' own pairs (alpha-box binning, what the blend processed): the same stream-ordered
             # frames replayed untimed, each one's count read after it (ptgs_splat_status last_pairs; the pairs
             # depend only on the camera), and the front end each frame took
@@ -545,6 +614,8 @@ def main():
                                      "splat_pairs_per_s": round(sum(opairs) / (odt * len(orbit)) / 1e9, 4),
                                      "static_splat_pairs_per_s": out["gs"]["splat_pairs_per_s"],
                                      "fused_frames": ofused,
+                                     "serial": {"value": round(N / odt_serial / 1e9, 4), "unit": "Gsplats/s",
+                                                "ms_per_step": round(odt_serial * 1e3, 4)},
                                      "pairs_K_range": [min(ks), max(ks)],
                                      "workload": f"C2 Gaussians, {len(orbit)} frames orbiting the cloud (1.5 deg per frame) "
                                                  "while dollying from 8 to 5 units and back, stream-ordered"}

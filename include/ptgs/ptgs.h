@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define PTGS_ABI_VERSION 3  /* 3: ptgs_gaussians.ids, ptgs_splat_stats.fused, ptgs_splat_status spill fields */
+#define PTGS_ABI_VERSION 4  /* 3: ptgs_gaussians.ids, ptgs_splat_stats.fused, ptgs_splat_status spill fields;
+                             * 4: PTGS_EBADIDS, PTGS_FLAG_SPLAT_OVERLAP */
 
 /* ---------------- error codes ---------------- */
 #define PTGS_OK 0
@@ -45,11 +46,16 @@ extern "C" {
 #define PTGS_EINCOMPLETE (-6) /* an EARLIER stream-ordered splat frame of this context could not be completed
                                * (its spill pool was exhausted: some tiles were left at the background).
                                * Returned once, by the first splat call that starts after that frame has
-                               * finished on the device; that call has grown the pool to 1.25x the latest
-                               * pair count published (which bounds the reported frame's spilled pairs) and
+                               * finished on the device; that call has grown the pool to 1.25x the largest
+                               * pair count any frame of the workspace has had (which bounds the reported
+                               * frame's spilled pairs) and
                                * rendered its own frame completely unless its own spilled tiles need more.
                                * ptgs_splat_gaussians_views renders every view before it returns the code.
                                * ptgs_splat_reserve prevents it (see there). */
+#define PTGS_EBADIDS (-7) /* an EARLIER stream-ordered splat frame of this context met ptgs_gaussians.ids
+                           * entries >= count (those Gaussians were dropped). Returned once, like
+                           * PTGS_EINCOMPLETE, by a call that has rendered its own frame; a code of its
+                           * own so a caller can tell it from this call's PTGS_EINVAL. */
 
 /* ---------------- reference struct layouts (Appendix B of SURVEY.md) ---------------- */
 

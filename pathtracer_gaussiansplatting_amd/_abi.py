@@ -10,15 +10,16 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptgs.so")
 
 PTGS_OK = 0
 ERRORS = {-1: "PTGS_EINVAL", -2: "PTGS_EHIP", -3: "PTGS_ENOSCENE", -4: "PTGS_ERANGE", -5: "PTGS_EIO",
-          -6: "PTGS_EINCOMPLETE"}
+          -6: "PTGS_EINCOMPLETE", -7: "PTGS_EBADIDS"}
 PTGS_EINVAL = -1
 PTGS_EINCOMPLETE = -6
+PTGS_EBADIDS = -7  # an earlier splat frame met ids >= count
 ACCUM_RUNNING_MEAN = 0
 ACCUM_SUM = 1
 FLAG_COUNT_TRAVERSAL = 1

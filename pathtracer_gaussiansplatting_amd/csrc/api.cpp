@@ -63,6 +63,7 @@ struct ptgs_ctx {
   hipEvent_t ov_call[PTGS_OV_RING] = {}, ov_done = nullptr;
   uint32_t ov_pos = 0;      // ring slot of the latest overlapped call
   uint32_t ov_depth = 0;    // workspaces in use (2 .. PTGS_OV_RING)
+  uint32_t pending_report = 0;  // earlier frames' reports a failing splat call collected (returned by the next)
   uint32_t ov_started = 0;  // consecutive overlapped calls so far (their ov_call events are valid)
   ptgs::WfWorkspace wf;  // wavefront path tracer buffers (PTGS_FLAG_PT_WAVEFRONT)
   ptgs::PtSched pt_sched;  // megakernel tile schedule (heavy tiles first)
@@ -723,8 +724,21 @@ static int splat_render(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
 }
 
 // (the frames of this call are rendered; the codes report earlier frames of the workspace(s))
+static int splat_report(ptgs_ctx* c, uint32_t report);
+// The reports a call collected (earlier frames' flags, consumed from the workspaces) and its own result:
+// a failing call keeps them for the next call (they are returned once, never dropped); a
+// successful one returns them together with any kept earlier.
+static int splat_finish(ptgs_ctx* c, int rc, uint32_t report) {
+  report |= c->pending_report;
+  c->pending_report = 0;
+  if (rc != PTGS_OK) {
+    c->pending_report = report;
+    return rc;
+  }
+  return splat_report(c, report);
+}
 static int splat_report(ptgs_ctx* c, uint32_t report) {
-  if (report & 2u) return fail(c, PTGS_EINVAL, "an earlier splat frame met ptgs_gaussians.ids entries >= count");
+  if (report & 2u) return fail(c, PTGS_EBADIDS, "an earlier splat frame met ptgs_gaussians.ids entries >= count");
   if (report & 1u)
     return fail(c, PTGS_EINCOMPLETE, "an earlier splat frame left tiles incomplete (spill pool exhausted; grown)");
   return PTGS_OK;
@@ -806,7 +820,7 @@ static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
   }
   const int rc = splat_render(c, g, ubo, w, h, bg, depth, under, tile_row_begin, tile_row_end, out, stats, stream,
                               &report, ovp);
-  return rc != PTGS_OK ? rc : splat_report(c, report);
+  return splat_finish(c, rc, report);
 }
 
 int ptgs_splat_gaussians(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
@@ -859,7 +873,10 @@ int ptgs_splat_gaussians_views(ptgs_ctx* c, const ptgs_gaussians* g, uint32_t n_
   };
   for (uint32_t v = 1; v < n_views; ++v) {
     hipError_t e = hipStreamWaitEvent(c->view_stream[v], c->view_fork, 0);
-    if (e != hipSuccess) { join(); return fail(c, PTGS_EHIP, "hipStreamWaitEvent: %s", hipGetErrorString(e)); }
+    if (e != hipSuccess) {
+      join();
+      return splat_finish(c, fail(c, PTGS_EHIP, "hipStreamWaitEvent: %s", hipGetErrorString(e)), report);
+    }
     SplatWorkspace* keep = c->splat;
     c->splat = c->view_ws[v];
     uint32_t rep = 0;
@@ -870,13 +887,13 @@ int ptgs_splat_gaussians_views(ptgs_ctx* c, const ptgs_gaussians* g, uint32_t n_
     // (record the join even after a failed view: kernels it did enqueue must be waited for)
     e = hipEventRecord(c->view_join[v], c->view_stream[v]);
     if (e == hipSuccess) launched = v + 1;
-    if (rc != PTGS_OK) { join(); return rc; }
-    if (e != hipSuccess) { join(); return fail(c, PTGS_EHIP, "hipEventRecord: %s", hipGetErrorString(e)); }
+    if (rc != PTGS_OK) { join(); return splat_finish(c, rc, report); }
+    if (e != hipSuccess) { join(); return splat_finish(c, fail(c, PTGS_EHIP, "hipEventRecord: %s", hipGetErrorString(e)), report); }
   }
   uint32_t rep = 0;
   const int rc = splat_render(c, g, &ubos[0], w, h, bg, nullptr, nullptr, 0, ~0u, outs[0], nullptr, stream, &rep);
   join();
-  return rc != PTGS_OK ? rc : splat_report(c, report | rep);
+  return splat_finish(c, rc, report | rep);
 }
 
 int ptgs_gaussians_sort_spatial(ptgs_ctx* c, const ptgs_gaussians* g, float* means, float* scales, float* rotations,

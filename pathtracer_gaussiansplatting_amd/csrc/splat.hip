@@ -75,7 +75,8 @@ struct SplatWorkspace {
   bool last_fused = false;    // the last frame ran the fused front end
   uint32_t* k_host = nullptr;  // pinned, coherent [16]: K, largest tile, large tiles, -, touched runs,
                                // fused overflow, publishing path (1 fused / 2 three), -, spill demand,
-                               // incomplete tile, bad ids, queued front-end slices
+                               // incomplete tile, bad ids, queued front-end slices, largest K (fused),
+                               // largest K (three launches)
   uint32_t* k_dev = nullptr;   // its device-side address
   hipEvent_t k_event = nullptr;
   uint32_t last_n = 0, last_k = 0, last_tiles = 0;
@@ -995,6 +996,8 @@ __global__ __launch_bounds__(GS_BIN_THREADS) void gs_bin_scatter_kernel(
     __atomic_store_n(k_host + 5, 0u, __ATOMIC_RELAXED);
     __atomic_store_n(k_host + 6, 2u, __ATOMIC_RELAXED);  // published by: three launches
     __atomic_store_n(k_host, carry, __ATOMIC_RELAXED);  // pinned host word: the host's K read-back
+    if (carry > total[2]) total[2] = carry;  // the workspace's largest K (three launches; fused: fz[13])
+    __atomic_store_n(k_host + 13, total[2], __ATOMIC_RELAXED);
     __threadfence_system();  // visible to the host before the kernel ends (the K event has no system fence)
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && (bg.row0 > 0 || bg.row1 < bg.grid_y)) {
@@ -2049,6 +2052,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
       __atomic_store_n(fu.k_host + 5, fu.fz[5], __ATOMIC_RELAXED);                  // tiles above scap (spilled)
       __atomic_store_n(fu.k_host + 6, 1u, __ATOMIC_RELAXED);                       // published by: fused
       __atomic_store_n(fu.k_host, fp, __ATOMIC_RELAXED);
+      if (fp > fu.fz[13]) fu.fz[13] = fp;  // the workspace's largest K (fused; three launches: total[2])
+      __atomic_store_n(fu.k_host + 12, fu.fz[13], __ATOMIC_RELAXED);
       fu.fz[1] = 0;
       fu.fz[4] = 0;
       fu.fz[5] = 0;
@@ -2560,10 +2565,11 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1u << 20, n), w->sp_cap);
     if (demand > w->sp_cap) want = std::max<uint64_t>(want, (uint64_t)demand + demand / 4u);
     // a reported frame's own demand reaches k_host[8] only with the NEXT front end: its spilled
-    // tiles hold at most its pair count, which its blend (running or done: it raised the report) has
-    // published to k_host[0], so the pool grows to that now and this frame cannot exhaust it the same way
+    // tiles hold at most its pair count, which is at most the largest K any frame of the workspace has
+    // published (k_host[12] fused, [13] three launches: device-side running maxima, so a later lighter frame
+    // cannot hide it), so the pool grows to that now and this frame cannot exhaust it the same way
     if (*report & 1u) {
-      const uint32_t k = w->k_host[0];
+      const uint32_t k = std::max({w->k_host[0], w->k_host[12], w->k_host[13]});
       want = std::max<uint64_t>(want, (uint64_t)k + k / 4u);
     }
     want = std::min<uint64_t>(want, 0xFFFFFFF0u);

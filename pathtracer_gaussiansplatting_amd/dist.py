@@ -185,7 +185,7 @@ def render_path_traced_frame(renderer, ubo, width: int, height: int, accum, spp_
 
 
 class _DeferredReport:
-    """PTGS_EINCOMPLETE / PTGS_EINVAL from a splat call report an EARLIER frame (ptgs.h): this call's frame
+    """PTGS_EINCOMPLETE / PTGS_EBADIDS from a splat call report an EARLIER frame (ptgs.h): this call's frame
     was rendered. Raising it before the frame's collective would leave the other ranks blocked in it (a
     multi-rank hang), so the splat calls of a sharded frame run inside this context, which holds
     such a report until the collective has been issued (`raise_pending`). Any other error raises at once."""
@@ -197,9 +197,9 @@ class _DeferredReport:
         return self
 
     def __exit__(self, et, ev, tb):
-        from ._abi import PTGS_EINCOMPLETE, PTGS_EINVAL, PtgsError
-        if et is not None and issubclass(et, PtgsError) and ev.code in (PTGS_EINCOMPLETE, PTGS_EINVAL) \
-                and "earlier splat frame" in str(ev):
+        from ._abi import PTGS_EBADIDS, PTGS_EINCOMPLETE, PtgsError
+        # (codes of their own for reports about earlier frames: no message matching)
+        if et is not None and issubclass(et, PtgsError) and ev.code in (PTGS_EINCOMPLETE, PTGS_EBADIDS):
             self.err = ev
             return True
         return False

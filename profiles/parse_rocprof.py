@@ -28,6 +28,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # kernels bench.py reports a roofline for: short key -> substring of the demangled name
 TRACKED = {"pt_camera_kernel": "pt_camera_kernel<false", "gs_sort_blend_kernel": "gs_sort_blend_kernel<false",
+           "gs_bin_fused_kernel": "gs_bin_fused_kernel<false, 512", "gs_bin_fused_kernel_ov": "gs_bin_fused_kernel<false, 256",
            "pt_extend_kernel": "pt_extend_kernel", "pt_shade_kernel": "pt_shade_kernel",
            "pt_shadow_kernel": "pt_shadow_kernel", "pt_raygen_kernel": "pt_raygen_kernel"}
 

@@ -33,7 +33,7 @@ def test_every_declared_symbol_is_exported(native_lib):
 
 
 def test_abi_version_and_arch(native_lib):
-    assert native_lib.ptgs_abi_version() == 3  # 3: ids / fused / the splat status's spill fields
+    assert native_lib.ptgs_abi_version() == 4  # 4: PTGS_EBADIDS, PTGS_FLAG_SPLAT_OVERLAP (3: ids / fused / spill fields)
     assert native_lib.ptgs_device_arch() == b"gfx950"
 
 

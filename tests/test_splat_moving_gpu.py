@@ -296,9 +296,10 @@ def test_gaussians_views_pool_exhausted_renders_every_view(native_lib):
 
 def test_gaussians_out_of_range_ids_are_reported(native_lib, oracle_lib):
     """ids must be a permutation of [0, N). An id >= N is never used as an index (the
-    Gaussian is dropped: no out-of-bounds write) and the next call returns PTGS_EINVAL."""
+    Gaussian is dropped: no out-of-bounds write) and the next call returns PTGS_EBADIDS (its own code:
+    a report about an earlier frame, not this call's PTGS_EINVAL)."""
     from pathtracer_gaussiansplatting_amd import Renderer, PtgsError
-    from pathtracer_gaussiansplatting_amd._abi import PTGS_EINVAL
+    from pathtracer_gaussiansplatting_amd._abi import PTGS_EBADIDS
     W, H, n = 160, 96, 2000
     g = Y.gaussians_c2(n, seed=47)
     ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
@@ -313,7 +314,7 @@ def test_gaussians_out_of_range_ids_are_reported(native_lib, oracle_lib):
         torch.cuda.synchronize()
         with pytest.raises(PtgsError) as ei:
             r.splat_gaussians(dict(dg, ids=good), ubo, W, H, out)
-        assert ei.value.code == PTGS_EINVAL
+        assert ei.value.code == PTGS_EBADIDS
         r.splat_gaussians(dict(dg, ids=good), ubo, W, H, out)
         torch.cuda.synchronize()
         ref = oracle_lib.splat_gaussians(g, ubo, W, H)
