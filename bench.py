@@ -100,6 +100,58 @@ def _roofline(kernel: str, traffic, kernel_ms: float, prof, cache_inclusive: dic
     return r
 
 
+def band_split_leg(r, Renderer, g, ubo, W, H, img, full_ms, stream, ranks=8, frames=10):
+    """The 8-GPU tile-row split of a large splat frame, rehearsed on this GPU: the
+    Gaussians' Morton copy with chunk bounds (what each rank renders from), rows balanced by a full frame's
+    per-row pair counts (dist.balanced_tile_rows), then re-split once from the measured band times
+    (dist.rebalance_tile_rows, two feedback steps, the better kept); each band on a context of its own (a rank renders its band every frame),
+    timed one after another. The 8-GPU frame is bounded below by the slowest band (plus the row gather,
+    ~16.6 MB per rank at 4K, overlapped by RowGatherPipeline). Unmeasured on 8 GPUs: no such node here."""
+    import torch
+    from pathtracer_gaussiansplatting_amd import dist as D
+    dg = r.sort_gaussians_spatial(g, stream=stream)
+    dg = dict(dg, chunk_bounds=r.gaussians_chunk_bounds(dg, stream=stream))
+    rp = Renderer(r.device, publish_splat_buffers=True)
+    st = rp.splat_gaussians(dg, ubo, W, H, img, want_stats=True, stream=stream)
+    b = rp.splat_buffers()
+    rng = np.zeros(2 * b.num_tiles, np.uint32)
+    rp.copy_d2h(rng, b.tile_ranges, rng.nbytes)
+    rp.close()
+    row_pairs = D.row_pairs_from_ranges(rng, st.tiles_x)
+    split = D.balanced_tile_rows(row_pairs, ranks, st.tiles_x)
+
+    def time_split(sp):
+        ms = []
+        for rows in sp:
+            rk = Renderer(r.device)
+            rk.splat_reserve(int(st.num_rendered))
+            for _ in range(6):
+                rk.splat_gaussians(dg, ubo, W, H, img, tile_rows=tuple(rows), stream=stream)
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(frames):
+                rk.splat_gaussians(dg, ubo, W, H, img, tile_rows=tuple(rows), stream=stream)
+            torch.cuda.synchronize()
+            ms.append((time.perf_counter() - t0) / frames * 1e3)
+            rk.close()
+        return ms
+
+    ms0 = time_split(split)
+    split1 = D.rebalance_tile_rows(split, ms0, row_pairs, st.tiles_x)
+    ms1 = time_split(split1)
+    split2 = D.rebalance_tile_rows(split1, ms1, row_pairs, st.tiles_x)  # (a second feedback step)
+    ms2 = time_split(split2)
+    if max(ms2) < max(ms1):
+        split1, ms1 = split2, ms2
+    del dg
+    return {"ranks": ranks, "rows_by_pairs": split, "band_ms_by_pairs": [round(x, 4) for x in ms0],
+            "rows_rebalanced": split1, "band_ms_rebalanced": [round(x, 4) for x in ms1],
+            "slowest_band_ms": round(max(ms1), 4), "full_frame_ms": round(full_ms, 4),
+            "full_over_slowest": round(full_ms / max(ms1), 3),
+            "note": "one GPU, bands one after another (Morton copy + chunk bounds); the 8-GPU frame itself is "
+                    "unmeasured (no 8-GPU node in this pool)"}
+
+
 def log2ceil(n):
     return max(0, math.ceil(math.log2(max(n, 1))))
 
@@ -373,7 +425,25 @@ def main():
         torch.cuda.synchronize()
         gsteps = max(args.steps, 100)  # ~0.1 ms per frame: enough frames for a stable mean
         gs_rows = None
+        gs_policy = "single"
+        gubo_rank = gubo
         if world > 1:
+            # how the ranks split C2 frames (dist.splat_policy): tile rows only when a rank's band
+            # outlasts rank 0's intake of the rows over xGMI; at C2 a band is ~7 us against ~83 us of gather,
+            # so each rank renders whole frames of its own view (replicas, the capture loop's many views)
+            for _ in range(20):
+                r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(50):
+                r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
+            torch.cuda.synchronize()
+            full_ms = max_over_ranks((time.perf_counter() - t1) / 50 * 1e3)
+            gs_policy = D.splat_policy(full_ms, W, H, world)
+            # (replicas: rank r's view turns the C2 camera by 360 r / world degrees about the cloud's centre)
+            th = 2.0 * math.pi * rank / world
+            gubo_rank = make_ubo(Camera(aspect=W / H).look_at([8.0 * math.sin(th), 0.0, -8.0 + 8.0 * math.cos(th)],
+                                                              [0.0, 0.0, -8.0]), cornell_box_scene(), 0)
             # SURVEY 8e tile-row shard: rows balanced by a full frame's per-row pair counts (the same
             # split on every rank), each rank renders its rows, rank 0 gathers them (W*H*16/G B each)
             st0 = r.splat_gaussians(dg, gubo, W, H, img, want_stats=True, stream=stream)
@@ -387,9 +457,13 @@ def main():
             gs_pipe = D.RowGatherPipeline(r, W, H, gs_rows, rank, world, stream=stream) if native_comm else None
 
         def gs_step():
-            if world == 1:
-                r.splat_gaussians(dg, gubo, W, H, img, stream=stream)
-            elif native_comm:
+            if world == 1 or gs_policy == "replicas":
+                r.splat_gaussians(dg, gubo_rank, W, H, img, stream=stream)
+            else:
+                gs_step_tiles()
+
+        def gs_step_tiles():
+            if native_comm:
                 gs_pipe.submit(dg, gubo)
             else:  # gloo rehearsal: the rows through host memory
                 if gs_rows[rank][1] > gs_rows[rank][0]:
@@ -413,7 +487,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(gsteps):  # timed: no per-stage events, no stats read-back
             gs_step()
-        if world > 1 and native_comm:
+        if gs_policy == "tile_rows" and native_comm:
             gs_pipe.wait()  # (the last frames' gathers are inside the timed region)
         torch.cuda.synchronize()
         barrier()
@@ -445,16 +519,38 @@ def main():
             t0 = time.perf_counter()
             for _ in range(gsteps):
                 gs_step()
-            if world > 1 and native_comm:
+            if gs_policy == "tile_rows" and native_comm:
                 gs_pipe.wait()
             torch.cuda.synchronize()
             barrier()
             sdt = max_over_ranks(time.perf_counter() - t0)
             assert_complete(r, "C2 serial loop")
-            gs_serial = {"value": round(args.gaussians / (sdt / gsteps) / 1e9, 4),
+            gs_serial = {"value": round(args.gaussians * (world if gs_policy == "replicas" else 1) / (sdt / gsteps) / 1e9, 4),
                          "unit": "Gsplats/s", "ms_per_step": round(sdt / gsteps * 1e3, 4),
                          "frame_latency_ms": round(frame_latency_ms(), 4),
                          "note": "one frame at a time on the caller's stream (front end, then blend)"}
+        gs_tiles = None
+        if gs_policy == "replicas":  # the tile-row shard of the same frame (secondary: the north_star's split)
+            r.set_splat_overlap(gs_overlap)
+            for _ in range(20):
+                gs_step_tiles()
+            if native_comm:
+                gs_pipe.wait()
+            torch.cuda.synchronize()
+            r.splat_status(stream)
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(gsteps):
+                gs_step_tiles()
+            if native_comm:
+                gs_pipe.wait()
+            torch.cuda.synchronize()
+            barrier()
+            tdt = max_over_ranks(time.perf_counter() - t0)
+            assert_complete(r, "C2 tile-row shard")
+            gs_tiles = {"value": round(args.gaussians / (tdt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
+                        "ms_per_step": round(tdt / gsteps * 1e3, 4), "scaling": "strong", "rows": gs_rows,
+                        "note": "one C2 frame split by tile rows balanced by pair counts + row gather to rank 0"}
         r.set_splat_overlap(False)
         # the same frames from the Gaussians in their generated (random) order: the same image bit for
         # bit, timed alone (secondary figure)
@@ -500,7 +596,8 @@ def main():
         b_gs = N * (56 + 48) + N * 48 + K * 12 + P * K * 24 + K * (4 + 48) + W * H * 16
         gms = gdt / gsteps * 1e3
         out["gs"] = {
-            "value": round(N / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(gms, 4),
+            "value": round(N * (world if gs_policy == "replicas" else 1) / (gdt / gsteps) / 1e9, 4), "unit": "Gsplats/s",
+            "ms_per_step": round(gms, 4),
             "frames_in_flight": ("on: each call's front end on the context's second stream beside the previous calls' "
                                  "blends (PTGS_FLAG_SPLAT_OVERLAP, 3 workspaces), every frame fully rendered")
             if gs_overlap else "off",
@@ -510,10 +607,16 @@ def main():
             "pairs_K_3sigma": K_exact,
             "skipped_frames": 0,  # incomplete frames: checked after every timed splat loop (ptgs_splat_status_read)
             "spilled_tiles": c2_spilled,
-            "scaling": "strong", "parallelism": "single GPU" if world == 1 else
-            f"tile-row shard x{world} (rows balanced by pair counts: {gs_rows}) + row gather to rank 0"
-            + (" (ptgs_gather_rows, RCCL, on a second stream: frame f's gather overlaps frame f + 1's band)"
-               if native_comm else " (gloo rehearsal, host copies)"),
+            "scaling": "weak" if gs_policy == "replicas" else "strong",
+            "policy": gs_policy,
+            "parallelism": "single GPU" if world == 1 else
+            (f"replicas x{world}: each rank renders whole frames of its own view (dist.splat_policy: a C2 band "
+             "would be shorter than rank 0's row intake over xGMI); nothing crosses the links"
+             if gs_policy == "replicas" else
+             f"tile-row shard x{world} (rows balanced by pair counts: {gs_rows}) + row gather to rank 0"
+             + (" (ptgs_gather_rows, RCCL, on a second stream: frame f's gather overlaps frame f + 1's band)"
+                if native_comm else " (gloo rehearsal, host copies)")),
+            "tile_shard": gs_tiles,
             "front_end": "fused single launch" if gstat.fused else "count + colscan + scatter",
             # per-stage split: kernel-trace averages of this libptgs.so when profiled (profiles/traffic_latest.json),
             # else per-stage HIP events of an untimed serial pass (each event pair adds its launch gap: the stages
@@ -550,7 +653,7 @@ def main():
             "time_basis": "rocprofv3 kernel-trace average of this libptgs.so (profiles/traffic_latest.json)" if bprof
                           else "per-stage HIP events (untimed serial pass)",
             "note": "algorithmic: 8-B key + 48-B blend record per (Gaussian, tile) pair + 16 B per pixel"})
-        out["gs"]["splat_pairs_per_s"] = round(K / (gdt / gsteps) / 1e9, 4)  # (Gaussian, tile) instances, G/s
+        out["gs"]["splat_pairs_per_s"] = round(K * (world if gs_policy == "replicas" else 1) / (gdt / gsteps) / 1e9, 4)
         if world == 1 and not args.headline_only:
             # four views of the C2 Gaussians per call (ptgs_splat_gaussians_views: forked streams, one
             # workspace per view), the capture-loop use: aggregate Gaussians x views per second
@@ -678,6 +781,8 @@ def main():
             out["gs_10m_4k"] = {"workload": f"C5 splat on one GPU: {N5} C2-distributed Gaussians, {W5}x{H5}",
                                 "value": round(N5 / d5 / 1e9, 4), "unit": "Gsplats/s", "ms_per_step": round(d5 * 1e3, 3),
                                 "pairs_K": int(st5.num_rendered)}
+            if not args.headline_only:
+                out["gs_10m_4k"]["bands8"] = band_split_leg(r, Renderer, g5, g5ubo, W5, H5, img5, d5 * 1e3, stream)
             del g5, img5
         if args.no_pt:
             out.update({"value": out["gs"]["value"], "unit": "Gsplats/s", "ms_per_step": out["gs"]["ms_per_step"],

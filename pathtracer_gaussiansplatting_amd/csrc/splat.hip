@@ -1990,6 +1990,8 @@ __device__ const uint32_t* gs_spill_tile(const GsSpill& sp, uint32_t tx, uint32_
 // chain, the termination applied without its wave-uniform branch, an XCD-aware tile mapping, loading the
 // key row only up to the previous frame's count, non-temporal records / key rows.
 #define GS_DONE_EVERY 4u  // list entries between the wave's all-pixels-done tests (a power of two >= 4)
+// (the termination as two selects per entry instead of the wave-uniform branch: 2 spilled VGPRs, C2 serial
+// 0.0607 vs 0.0563 ms, round 6)
 // (Measured and rejected, round 6: the quadratic as three packed v_pk_mul / v_pk_fma_f32 over the record's
 // (A, C) (B, D) (E, F) pairs plus one add, and red / green as one packed FMA: 13 VALU per entry instead of
 // 15, but C2 0.0574 vs 0.0558 ms: the packed ops' dependency stalls (s_nop) lengthen each wave's chain.)

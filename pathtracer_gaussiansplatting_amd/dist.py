@@ -40,7 +40,27 @@ def balanced_tile_rows(row_pairs, world: int, tiles_x: int, tile_cost: float = 3
     (Gaussian, tile) pairs plus tile_cost per tile (the per-tile fixed work). row_pairs: pairs per
     tile row (e.g. from a previous frame's tile ranges)."""
     import numpy as np
+    return _split_rows(np.asarray(row_pairs, np.float64) + tile_cost * tiles_x, world)
+
+
+def rebalance_tile_rows(split, band_ms, row_pairs, tiles_x: int, tile_cost: float = 32.0) -> list[tuple[int, int]]:
+    """Re-split tile rows from measured band times (a multi-GPU renderer times each rank's band every frame:
+    pair counts alone miss what else a band costs, e.g. the chunks its front end keeps). Each row of band b
+    is given band_ms[b] x its share of the band's pair-based weight (balanced_tile_rows' weights) and the
+    cumulative cost is cut into equal parts again. 10M Gaussians at 4K, 8 bands: slowest band 1.451 ms from
+    the pair split (bands 1.156 - 1.451 ms), see DESIGN §6."""
+    import numpy as np
     w = np.asarray(row_pairs, np.float64) + tile_cost * tiles_x
+    cost = np.zeros_like(w)
+    for (a, b), ms in zip(split, band_ms):
+        if b > a:
+            cost[a:b] = float(ms) * w[a:b] / max(w[a:b].sum(), 1e-30)
+    return _split_rows(cost, len(split))
+
+
+def _split_rows(w, world: int) -> list[tuple[int, int]]:
+    """Contiguous row ranges, one per rank, of about equal total weight (w: per row)."""
+    import numpy as np
     rows = len(w)
     cum = np.concatenate([[0.0], np.cumsum(w)])
     bounds = [0]
@@ -52,6 +72,20 @@ def balanced_tile_rows(row_pairs, world: int, tiles_x: int, tile_cost: float = 3
         bounds.append(min(max(b, bounds[-1]), rows))
     bounds.append(rows)
     return [(bounds[g], bounds[g + 1]) for g in range(world)]
+
+
+def splat_policy(frame_ms: float, width: int, height: int, world: int, link_gbs: float = 50.0) -> str:
+    """How several GPUs split 3DGS frames: "tile_rows" (every rank renders a band of each frame,
+    rank 0 gathers the rows) when a rank's share of the frame (frame_ms / world, the ideal band) takes longer
+    than rank 0's intake of a peer's rows over its own xGMI link (W*H*16/world bytes at link_gbs per link,
+    all peers in parallel); else "replicas" (each rank renders whole frames of its own - other views or
+    other frames - and nothing crosses the links). C2 (100k Gaussians, 1080p, ~0.053 ms): the band would be
+    ~7 us against ~83 us of gather at 8 ranks -> replicas; C5's splat (10M Gaussians, 4K, ~8.5 ms): ~1.07 ms
+    against ~0.33 ms -> tile rows. world 1: "single"."""
+    if world <= 1:
+        return "single"
+    gather_ms = width * height * 16.0 / world / (link_gbs * 1e9) * 1e3
+    return "tile_rows" if frame_ms / world > gather_ms else "replicas"
 
 
 def row_pairs_from_ranges(tile_ranges, tiles_x: int):

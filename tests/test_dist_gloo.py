@@ -386,3 +386,102 @@ def test_row_gather_pipeline_gloo():
         p.join(timeout=120)
     assert res[0] == "ok", res[1]
     assert res[1] == [True] * 4, res
+
+
+def test_splat_policy():
+    """DESIGN §6, VERDICT r5 next #3: how several GPUs split 3DGS frames. C2 (100k Gaussians, 1080p, one
+    frame ~0.053 ms on one GPU): a rank's band (~7 us at 8 ranks) is far shorter than rank 0's intake of a
+    peer's rows over one xGMI link (1920*1080*16/8 B at 50 GB/s ~ 83 us) -> replicas; C5's splat (10M
+    Gaussians, 3840x2160, ~8.5 ms) -> tile rows from 2 ranks on; one GPU -> single."""
+    from pathtracer_gaussiansplatting_amd import dist as D
+    assert D.splat_policy(0.053, 1920, 1080, 1) == "single"
+    for world in (2, 4, 8):
+        assert D.splat_policy(0.053, 1920, 1080, world) == "replicas"
+        assert D.splat_policy(8.5, 3840, 2160, world) == "tile_rows"
+    # the crossover: a band of frame_ms / world against W*H*16/world B at 50 GB/s
+    gather_ms = 1920 * 1080 * 16 / 50e9 * 1e3  # (x world / world)
+    assert D.splat_policy(gather_ms * 1.01, 1920, 1080, 8) == "tile_rows"
+    assert D.splat_policy(gather_ms * 0.99, 1920, 1080, 8) == "replicas"
+
+
+def _replica_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import math
+        import oracle
+        import scenes_util as U
+        from pathtracer_gaussiansplatting_amd import Camera, make_ubo
+        from pathtracer_gaussiansplatting_amd import dist as D
+        from pathtracer_gaussiansplatting_amd import synthetic as Y
+        g = Y.gaussians_c2(1500, seed=5)
+        W, H = 96, 70
+        # the policy from the slowest rank's frame time (bench.py: max over ranks), the same on every rank
+        t = torch.tensor([0.053 if rank == 0 else 0.051], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        policy = D.splat_policy(float(t.item()), 1920, 1080, world)
+        # replicas: rank r renders whole frames of its own view (bench.py's C2 leg at world > 1)
+        th = 2.0 * math.pi * rank / world
+        ubo = make_ubo(Camera(aspect=W / H).look_at([8.0 * math.sin(th), 0.0, -8.0 + 8.0 * math.cos(th)],
+                                                    [0.0, 0.0, -8.0]), U.cornell(), 0)
+        img = torch.from_numpy(oracle.splat_gaussians(g, ubo, W, H)["image"])
+        frames = torch.tensor([1.0])
+        dist.all_reduce(frames)  # (the whole job's frames: one per rank per step)
+        outs = [torch.zeros_like(img) for _ in range(world)] if rank == 0 else None
+        dist.gather(img, outs, dst=0)  # (test only: each rank's frame checked on rank 0)
+        if rank == 0:
+            ok = []
+            for rr in range(world):
+                th2 = 2.0 * math.pi * rr / world
+                u2 = make_ubo(Camera(aspect=W / H).look_at([8.0 * math.sin(th2), 0.0, -8.0 + 8.0 * math.cos(th2)],
+                                                           [0.0, 0.0, -8.0]), U.cornell(), 0)
+                ok.append(bool(np.array_equal(outs[rr].numpy(), oracle.splat_gaussians(g, u2, W, H)["image"])))
+            distinct = not np.array_equal(outs[0].numpy(), outs[1].numpy())
+            q.put(("ok", policy, float(frames.item()), ok, distinct))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", traceback.format_exc()))
+
+
+def test_splat_replicas_gloo(oracle_lib, native_lib):
+    """The C2 policy at small N (world 2, gloo, the oracle as each rank's renderer): every rank picks
+    "replicas" from the same (max-over-ranks) frame time and renders whole frames of its own view; the views
+    differ, each frame equals the single-process render of that view, and the job renders world frames per
+    step with no image crossing between ranks in the timed path."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == "ok", res[1]
+    _, policy, frames, ok, distinct = res
+    assert policy == "replicas" and frames == world and all(ok) and distinct, res
+
+
+def test_rebalance_tile_rows():
+    """dist.rebalance_tile_rows: bands whose measured time exceeds the others' give rows away; a split whose
+    band times are equal is kept; the result covers every row once, in order."""
+    import numpy as np
+    from pathtracer_gaussiansplatting_amd import dist as D
+    row_pairs = np.full(40, 1000.0)
+    split = D.balanced_tile_rows(row_pairs, 4, 10)
+    assert split == [(0, 10), (10, 20), (20, 30), (30, 40)]
+    assert D.rebalance_tile_rows(split, [1.0, 1.0, 1.0, 1.0], row_pairs, 10) == split
+    # band 0 measured twice as slow: it shrinks, the others grow
+    new = D.rebalance_tile_rows(split, [2.0, 1.0, 1.0, 1.0], row_pairs, 10)
+    assert new[0][0] == 0 and new[-1][1] == 40 and all(a[1] == b[0] for a, b in zip(new, new[1:]))
+    assert new[0][1] - new[0][0] < 10 and new[-1][1] - new[-1][0] > 10, new
+    # the re-split's predicted band costs are about equal (rows of band 0 cost 0.2, the rest 0.1)
+    cost = np.where(np.arange(40) < 10, 0.2, 0.1)
+    per = [cost[a:b].sum() for a, b in new]
+    assert max(per) - min(per) <= 0.2 + 1e-9, per
