@@ -102,6 +102,12 @@ def main():
         stats("  records", sm[:, 6] - sm[:, 5])
         stats("  rank + stage + barrier", sm[:, 1] - sm[:, 6])
         stats("  evaluation", sm[:, 2] - sm[:, 1])
+    # workgroup lifetimes by position in the blend's (heavy-first) tile order: where the slot-time goes
+    life = (b[:, 3] - b[:, 0]) * 0.01
+    edges = [0, 1000, 2000, 3000, 4000, 5000, 6000, 7000, len(b)]
+    print("  lifetime by order position (workgroups: sum of lifetimes us, mean us): " + "; ".join(
+        f"[{a}, {e}): {life[a:e].sum():.0f}, {life[a:e].mean():.2f}" for a, e in zip(edges, edges[1:]) if e > a))
+    print(f"  sum of lifetimes {life.sum():.0f} us over {len(b)} workgroups (/ 2048 slots = {life.sum() / 2048:.2f} us)")
     # concurrency: workgroups resident over time
     ts = np.arange(b[:, 0].min(), b[:, 3].max(), 50)
     conc = [(np.count_nonzero((b[:, 0] <= t) & (b[:, 3] > t))) for t in ts]
