@@ -153,3 +153,52 @@ def test_band_3_of_8_at_10m_4k_vs_oracle(native_lib, oracle_lib, mode):
         print(f"10M 4K band {rows}: {ref['K']} pairs ({mode}) bit-exact, rel L2 {err:.2e}")
     finally:
         r.close()
+
+
+def test_balanced_bands_at_10m_4k_vs_oracle(native_lib, oracle_lib):
+    """the 8-rank split bench.py's band leg uses (rows balanced by a full frame's per-row
+    pair counts, dist.balanced_tile_rows): the eight bands' pair counts sum to the full frame's (the tile-row
+    partition loses and repeats nothing), and the heaviest band (the frame centre: the 8-GPU frame's
+    critical rank) equals the oracle's band bit for bit in the timed frames' binning."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    from pathtracer_gaussiansplatting_amd import dist as D
+    W, H, n = 3840, 2160, 10_000_000
+    g = Y.gaussians_c2(n, seed=5)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    r = Renderer(0, publish_splat_buffers="tight")
+    try:
+        dg = r.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        dgb = dict(dg, chunk_bounds=r.gaussians_chunk_bounds(dg))
+        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        st = r.splat_gaussians(dgb, ubo, W, H, out, want_stats=True)
+        torch.cuda.synchronize()
+        b = r.splat_buffers()
+        K_full = st.num_rendered
+        rng = _read(r, b.tile_ranges, 2 * b.num_tiles, np.uint32)
+        row_pairs = D.row_pairs_from_ranges(rng, st.tiles_x)
+        split = D.balanced_tile_rows(row_pairs, 8, st.tiles_x)
+        assert split[0][0] == 0 and split[-1][1] == st.tiles_y
+        assert all(a[1] == b_[0] for a, b_ in zip(split, split[1:]))
+        assert len({r1 - r0 for r0, r1 in split}) > 1, split  # (not the equal-rows split)
+        ks = []
+        for rows in split:
+            stb = r.splat_gaussians(dgb, ubo, W, H, out, tile_rows=tuple(rows), want_stats=True)
+            torch.cuda.synchronize()
+            ks.append(stb.num_rendered)
+        assert sum(ks) == K_full, (ks, K_full)
+        heavy = split[int(np.argmax(ks))]
+        ref = oracle_lib.splat_gaussians(g, ubo, W, H, tile_rows=tuple(heavy), tight=True)
+        for frame in range(2):
+            st = r.splat_gaussians(dgb, ubo, W, H, out, tile_rows=tuple(heavy), want_stats=True)
+            torch.cuda.synchronize()
+            b = r.splat_buffers()
+            assert st.num_rendered == ref["K"] == max(ks), (frame, st.num_rendered, ref["K"], ks)
+            np.testing.assert_array_equal(_read(r, b.sorted_keys, ref["K"], np.uint64), ref["keys"])
+            np.testing.assert_array_equal(_read(r, b.sorted_values, ref["K"], np.uint32), ref["vals"])
+            np.testing.assert_array_equal(_read(r, b.tile_ranges, 2 * b.num_tiles, np.uint32), ref["ranges"])
+        r0, r1 = heavy[0] * 16, min(heavy[1] * 16, H)
+        err = U.rel_l2(out[r0:r1].cpu().numpy(), ref["image"][r0:r1])
+        assert err < 1e-4, err
+        print(f"10M 4K balanced split {split}: band pairs {ks}; heaviest {tuple(heavy)} bit-exact, rel L2 {err:.2e}")
+    finally:
+        r.close()

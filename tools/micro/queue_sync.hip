@@ -7,6 +7,10 @@
 //   marker     A: record(eA) K                                                 (a marker alone)
 //   wait_mark  B: k_short record(eB);            A: wait(eB) record(eA) K     (the marker right behind the barrier)
 //   waitval    B: k_short writeValue(f);         A: waitValue(f >= frame) K   (stream memory operations)
+//   pingpong   frame f on Q = f odd ? B : A: k_short, wait(done of frame f - 1, the other queue), K, record(done_f)
+//              (whole frames alternate queues; the long kernels stay ordered through a pending barrier)
+//   pingpong_s pingpong plus the caller's stream S: S records a marker per frame that the frame's k_short
+//              waits for (the marker of frame f - 1) and S waits for done_f (the join of each frame)
 // each with device-scope (no system fence) and default events; and stream priorities for B.
 //   hipcc -O3 --offload-arch=gfx950 tools/micro/queue_sync.hip -o tools/micro/queue_sync && tools/micro/queue_sync
 #include <hip/hip_runtime.h>
@@ -38,9 +42,16 @@ int main() {
     hipEvent_t eA, eB;
     CHK(hipEventCreateWithFlags(&eA, fl));
     CHK(hipEventCreateWithFlags(&eB, fl));
-    const char* names[] = {"alone", "wait", "wait_only", "marker", "wait_mark", "waitval"};
+    const char* names[] = {"alone", "wait", "wait_only", "marker", "wait_mark", "waitval", "pingpong", "pingpong_s"};
     unsigned* flag = buf + 4096;
-    for (int mode = 0; mode < 6; ++mode) {
+    hipStream_t S;
+    CHK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
+    hipEvent_t done[2], sm[2];
+    for (int q = 0; q < 2; ++q) {
+      CHK(hipEventCreateWithFlags(&done[q], fl));
+      CHK(hipEventCreateWithFlags(&sm[q], fl));
+    }
+    for (int mode = 0; mode < 8; ++mode) {
       std::vector<double> us;
       for (int rep = 0; rep < 6; ++rep) {
         CHK(hipDeviceSynchronize());
@@ -62,6 +73,19 @@ int main() {
             CHK(hipStreamWriteValue32(B, flag, seq, 0));
             CHK(hipStreamWaitValue32(A, flag, seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
           }
+          if (mode >= 6) {
+            hipStream_t Q = (f & 1) ? B : A;
+            if (mode == 7) {
+              CHK(hipEventRecord(sm[f & 1], S));
+              if (f) CHK(hipStreamWaitEvent(Q, sm[(f - 1) & 1], 0));
+            }
+            hipLaunchKernelGGL(spin_kernel, dim3(64), dim3(256), 0, Q, 200ull, buf);
+            if (f) CHK(hipStreamWaitEvent(Q, done[(f - 1) & 1], 0));
+            hipLaunchKernelGGL(spin_kernel, dim3(2048), dim3(256), 0, Q, 2000ull, buf);
+            CHK(hipEventRecord(done[f & 1], Q));
+            if (mode == 7) CHK(hipStreamWaitEvent(S, done[f & 1], 0));
+            continue;
+          }
           hipLaunchKernelGGL(spin_kernel, dim3(2048), dim3(256), 0, A, 2000ull, buf);  // ~20 us
         }
         CHK(hipDeviceSynchronize());
@@ -72,6 +96,11 @@ int main() {
       printf("%-10s events %-12s: %.2f us per frame (median of %zu)\n", names[mode],
              fence ? "system-scope" : "device-scope", us[us.size() / 2], us.size());
     }
+    for (int q = 0; q < 2; ++q) {
+      CHK(hipEventDestroy(done[q]));
+      CHK(hipEventDestroy(sm[q]));
+    }
+    CHK(hipStreamDestroy(S));
     CHK(hipEventDestroy(eA));
     CHK(hipEventDestroy(eB));
     CHK(hipStreamDestroy(A));
