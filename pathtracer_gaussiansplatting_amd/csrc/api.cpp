@@ -37,8 +37,9 @@
 using namespace ptgs;
 
 // frames in flight of PTGS_FLAG_SPLAT_OVERLAP: workspaces in the ring (the front end of call k may run
-// beside the blends of calls k - 1 .. k - RING + 1; PTGS_GS_OV_DEPTH=2 uses two)
-#define PTGS_OV_RING 3
+// beside the blends of calls k - 1 .. k - depth + 1; PTGS_GS_OV_DEPTH=2 .. 4, default 3)
+#define PTGS_OV_RING 4        // workspaces the ring may hold (PTGS_GS_OV_DEPTH)
+#define PTGS_OV_DEPTH_DEFAULT 3
 
 struct ptgs_ctx {
   int device = 0;
@@ -56,15 +57,15 @@ struct ptgs_ctx {
   hipStream_t view_stream[PTGS_MAX_VIEWS] = {};
   hipEvent_t view_fork = nullptr, view_join[PTGS_MAX_VIEWS] = {};
   // PTGS_FLAG_SPLAT_OVERLAP: a ring of workspaces (`splat` is always the latest call's; ov_ring[0] is the
-  // context's own first workspace), the front-end stream, the caller's stream at the start of each of the
-  // last calls (ov_call[i]: the call that used ov_ring[i]), the front end's end
+  // context's own first workspace), the front-end stream, the caller's stream at the start of every
+  // (depth - 1)-th call (ov_call[0] / [1] alternately; see splat_overlap_begin), the front end's end
   SplatWorkspace* ov_ring[PTGS_OV_RING] = {};
   hipStream_t ov_stream = nullptr;
-  hipEvent_t ov_call[PTGS_OV_RING] = {}, ov_done = nullptr;
+  hipEvent_t ov_call[2] = {}, ov_done = nullptr;
   uint32_t ov_pos = 0;      // ring slot of the latest overlapped call
   uint32_t ov_depth = 0;    // workspaces in use (2 .. PTGS_OV_RING)
   uint32_t pending_report = 0;  // earlier frames' reports a failing splat call collected (returned by the next)
-  uint32_t ov_started = 0;  // consecutive overlapped calls so far (their ov_call events are valid)
+  uint32_t ov_started = 0;  // consecutive overlapped calls so far (0: the next one records and waits for its own marker)
   ptgs::WfWorkspace wf;  // wavefront path tracer buffers (PTGS_FLAG_PT_WAVEFRONT)
   ptgs::PtSched pt_sched;  // megakernel tile schedule (heavy tiles first)
   void* comm = nullptr;  // RCCL communicator (ptgs_comm_create)
@@ -744,16 +745,16 @@ static int splat_report(ptgs_ctx* c, uint32_t report) {
   return PTGS_OK;
 }
 
-// PTGS_FLAG_SPLAT_OVERLAP: the call takes the other workspace (the one of the call before the previous
-// one) and, for a stream-ordered frame, its front end runs on the context's second stream once the caller's
-// stream has finished what it held at the start of the previous call: that covers the workspace's last
-// frame (two calls ago, blend included) and the inputs the caller wrote before then. Without the flag
+// PTGS_FLAG_SPLAT_OVERLAP: the call takes the ring's next workspace (the one of the call depth calls back)
+// and, for a stream-ordered frame, its front end runs on the context's second stream once the caller's
+// stream has finished what it held at the start of one of the last depth - 1 calls: that covers the
+// workspace's last frame (blend included) and the inputs the caller wrote before then. Without the flag
 // the front end follows the caller's stream (ov_started is cleared: the next overlapped call starts
 // from the caller's stream as it is then).
-// workspaces in the ring, fixed when a context first overlaps (PTGS_GS_OV_DEPTH=2: two; A/B switch)
+// workspaces in the ring, fixed when a context first overlaps (PTGS_GS_OV_DEPTH=2 .. 4; A/B switch)
 static uint32_t overlap_depth() {
   const char* v = getenv("PTGS_GS_OV_DEPTH");
-  const int x = v ? atoi(v) : PTGS_OV_RING;
+  const int x = v ? atoi(v) : PTGS_OV_DEPTH_DEFAULT;
   return (uint32_t)std::max(2, std::min(x, PTGS_OV_RING));
 }
 
@@ -782,16 +783,22 @@ static int splat_overlap_begin(ptgs_ctx* c, hipStream_t s, SplatOverlap* ov) {
     const char* v = getenv("PTGS_GS_OV_FENCE");
     return (unsigned)(hipEventDisableTiming | (v && !strcmp(v, "1") ? 0u : (unsigned)hipEventDisableSystemFence));
   }();
-  for (hipEvent_t* ev : {&c->ov_call[0], &c->ov_call[1], &c->ov_call[2], &c->ov_done})
+  for (hipEvent_t* ev : {&c->ov_call[0], &c->ov_call[1], &c->ov_done})
     if (!*ev) HIPCHK(c, hipEventCreateWithFlags(ev, ev_flags));
-  // the next ring slot; the workspace there was last used depth calls ago, and the caller's stream at the
-  // start of the call after that one (depth - 1 calls ago) had finished it, blend included
+  // the next ring slot; the workspace there was last used depth calls ago. The front end waits for a
+  // marker of the caller's stream recorded at the start of one of the last depth - 1 calls (the caller's
+  // stream had finished the workspace's last frame there, blend included). Markers are recorded every
+  // depth - 1 calls only (into two alternating events): a marker beside the cross-queue barrier costs the
+  // caller's queue ~3 us per frame (tools/micro/queue_sync.hip: wait + marker 28.0 vs wait alone 25.1 us on a
+  // 22 us kernel), so the front end of call k waits for the marker of call m (k - 1) / m, m = depth - 1
+  // (call 0: its own), and sees the caller's work enqueued before the call depth - 1 calls back.
   const uint32_t cur = (c->ov_pos + 1) % depth;
   c->ov_pos = cur;
   c->splat = c->ov_ring[cur];
-  HIPCHK(c, hipEventRecord(c->ov_call[cur], s));
+  const uint32_t m = depth - 1, k = c->ov_started;
+  if (k % m == 0) HIPCHK(c, hipEventRecord(c->ov_call[(k / m) & 1u], s));
   ov->fe = c->ov_stream;
-  ov->wait = c->ov_started >= depth - 1 ? c->ov_call[(cur + 1) % depth] : c->ov_call[cur];
+  ov->wait = c->ov_call[k == 0 ? 0u : ((k - 1) / m) & 1u];
   ov->done = c->ov_done;
   // the blend's tile order: the front end's order workgroup from the workspace's previous frame (default),
   // or PTGS_GS_OV_ORDER=own: a launch behind the front end from the frame's own counts (A/B switch;
@@ -801,7 +808,7 @@ static int splat_overlap_begin(ptgs_ctx* c, hipStream_t s, SplatOverlap* ov) {
     return v && !strcmp(v, "own");
   }();
   ov->own_order = own_order;
-  c->ov_started = std::min(c->ov_started + 1u, (uint32_t)PTGS_OV_RING);
+  c->ov_started = k + 1u;  // (wraps to 0 after 2^32 calls: a call that waits for its own marker, safe)
   return PTGS_OK;
 }
 

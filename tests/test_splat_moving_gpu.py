@@ -436,7 +436,7 @@ def _overlap_frames(W, H):
     return f + f + [orbit_ubo(0, W, H)] * 4
 
 
-@pytest.mark.parametrize("depth", ["3", "2"])
+@pytest.mark.parametrize("depth", ["3", "2", "4"])
 def test_gaussians_overlapped_frames_equal_serial(native_lib, monkeypatch, depth):
     """PTGS_FLAG_SPLAT_OVERLAP (frames in flight: each call's front end on the context's second stream,
     beside the previous calls' blends, over a ring of workspaces). Every frame of a moving, spilling
@@ -457,7 +457,7 @@ def test_gaussians_overlapped_frames_equal_serial(native_lib, monkeypatch, depth
         outs_b = [torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda") for _ in frames]
         for k, ubo in enumerate(frames):
             ra.splat_gaussians(da, ubo, W, H, outs_a[k], bg=(0.1, 0.2, 0.3))
-            if k < 3:  # (each ring workspace's row size reaches the host: its later frames run fused)
+            if k < int(depth):  # (each ring workspace's row size reaches the host: its later frames run fused)
                 torch.cuda.synchronize()
         for k, ubo in enumerate(frames):
             rb.splat_gaussians(db, ubo, W, H, outs_b[k], bg=(0.1, 0.2, 0.3))

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The bench's gs_orbit camera path (C2 Gaussians, Morton copy with ids) frame by frame: pair count K,
-largest tile, front end, per-frame wall time of a stream-ordered run. GS_FRAMES (default 120).
-Run under rocprofv3 --kernel-trace to see the kernels per frame.
+largest tile, front end, per-frame wall time of a stream-ordered run. GS_FRAMES (default 120); GS_OVERLAP=1:
+frames in flight (PTGS_FLAG_SPLAT_OVERLAP). Run under rocprofv3 --kernel-trace to see the kernels per frame
+(tools/kt_overlap.py <dir> 6 240: the timed orbit's dispatches).
    tools/gs_orbit.py [libptgs variant]"""
 import os
 import sys
@@ -22,6 +23,7 @@ def main():
     W, H, n = 1920, 1080, 100_000
     frames = int(os.environ.get("GS_FRAMES", "120"))
     r = Renderer(0, lib_path=lib)
+    r.set_splat_overlap(os.environ.get("GS_OVERLAP", "0") == "1")
     dg = r.sort_gaussians_spatial({k: torch.from_numpy(a).cuda() for k, a in Y.gaussians_c2(n, seed=1).items()})
     ubos = bench.gs_orbit_ubos(Camera, make_ubo, cornell_box_scene(), W, H, frames)
     img = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")

@@ -7,6 +7,8 @@
 //   marker     A: record(eA) K                                                 (a marker alone)
 //   wait_mark  B: k_short record(eB);            A: wait(eB) record(eA) K     (the marker right behind the barrier)
 //   waitval    B: k_short writeValue(f);         A: waitValue(f >= frame) K   (stream memory operations)
+//   post_mark  B: k_short record(eB);            A: wait(eB) K record(eA)     (the marker behind the kernel)
+//   post_mark2 post_mark with the marker every second frame only
 //   pingpong   frame f on Q = f odd ? B : A: k_short, wait(done of frame f - 1, the other queue), K, record(done_f)
 //              (whole frames alternate queues; the long kernels stay ordered through a pending barrier)
 //   pingpong_s pingpong plus the caller's stream S: S records a marker per frame that the frame's k_short
@@ -42,7 +44,8 @@ int main() {
     hipEvent_t eA, eB;
     CHK(hipEventCreateWithFlags(&eA, fl));
     CHK(hipEventCreateWithFlags(&eB, fl));
-    const char* names[] = {"alone", "wait", "wait_only", "marker", "wait_mark", "waitval", "pingpong", "pingpong_s"};
+    const char* names[] = {"alone", "wait", "wait_only", "marker", "wait_mark", "waitval", "pingpong", "pingpong_s",
+                           "post_mark", "post_mark2"};
     unsigned* flag = buf + 4096;
     hipStream_t S;
     CHK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
@@ -51,7 +54,7 @@ int main() {
       CHK(hipEventCreateWithFlags(&done[q], fl));
       CHK(hipEventCreateWithFlags(&sm[q], fl));
     }
-    for (int mode = 0; mode < 8; ++mode) {
+    for (int mode = 0; mode < 10; ++mode) {
       std::vector<double> us;
       for (int rep = 0; rep < 6; ++rep) {
         CHK(hipDeviceSynchronize());
@@ -84,6 +87,14 @@ int main() {
             hipLaunchKernelGGL(spin_kernel, dim3(2048), dim3(256), 0, Q, 2000ull, buf);
             CHK(hipEventRecord(done[f & 1], Q));
             if (mode == 7) CHK(hipStreamWaitEvent(S, done[f & 1], 0));
+            continue;
+          }
+          if (mode >= 8) {
+            hipLaunchKernelGGL(spin_kernel, dim3(64), dim3(256), 0, B, 200ull, buf);
+            CHK(hipEventRecord(eB, B));
+            CHK(hipStreamWaitEvent(A, eB, 0));
+            hipLaunchKernelGGL(spin_kernel, dim3(2048), dim3(256), 0, A, 2000ull, buf);
+            if (mode == 8 || (f & 1)) CHK(hipEventRecord(eA, A));
             continue;
           }
           hipLaunchKernelGGL(spin_kernel, dim3(2048), dim3(256), 0, A, 2000ull, buf);  // ~20 us
