@@ -83,9 +83,16 @@ def main(tag, workload):
               "| kernel | VGPRs | dispatches | avg ms | FETCH KiB | WRITE KiB | HBM bytes (2F+W)·1024 | HBM GB/s | "
               "frac of 8 TB/s | L2 hit | VALU lanes | VALU issue | wave wait |",
               "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    # the hash of the library the box profiled (profile.sh writes it next to the traces); a run without it
+    # falls back to the local library, which must then be the one that was sent
+    sha_file = os.path.join(base, "lib_sha256.txt")
+    if os.path.exists(sha_file):
+        lib_sha = open(sha_file).read().split()[0]
+    else:
+        lib_sha = hashlib.sha256(open(os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", "libptgs.so"),
+                                      "rb").read()).hexdigest()
     out = {"tag": tag, "workload": workload,
-           "lib_sha256": hashlib.sha256(open(os.path.join(ROOT, "pathtracer_gaussiansplatting_amd", "libptgs.so"),
-                                             "rb").read()).hexdigest(),
+           "lib_sha256": lib_sha,
            "formula": {"hbm_bytes": "(2*FETCH_SIZE + WRITE_SIZE) * 1024", "l2_hit": "TCC_HIT/(TCC_HIT+TCC_MISS)",
                        "valu_lanes": "SQ_THREAD_CYCLES_VALU/(64*SQ_ACTIVE_INST_VALU)"},
            "kernels": {}}

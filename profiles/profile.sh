@@ -14,6 +14,7 @@ TAG=${1:-r02}
 ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --headline-only --no-cpu-baseline --no-hybrid --no-gs-1m --no-gs-10m --no-gpu-bvh --no-c1 --no-c5 --no-torus --no-capture"}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
+sha256sum pathtracer_gaussiansplatting_amd/libptgs.so > "$OUT/lib_sha256.txt"  # (the profiled library: traffic_latest.json)
 export TMPDIR=/tmp
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_kt.log" 2>&1
