@@ -437,13 +437,14 @@ typedef struct ptgs_trace_stats {
                                       * of the previous call, which still runs on hip_stream; the two calls
                                       * use a ring of three workspaces. The blend, i.e. everything written to
                                       * out_rgba32f, stays ordered on hip_stream exactly as without the flag.
-                                      * Contract: the front end of a call waits only for the work enqueued on
-                                      * hip_stream before the splat call TWO calls back (the ring's depth - 1)
-                                      * of the context, so inputs (Gaussians, ids, chunk bounds) written on the
-                                      * stream between calls must be followed by one call without this flag (or
-                                      * a synchronisation) — like a Vulkan frame in flight, whose resources the
-                                      * application does not touch. Same image, keys and counts as without the
-                                      * flag. */
+                                      * Contract: a run of overlapped calls (the first call with the flag, or
+                                      * the first after a splat call without it) starts after the work enqueued
+                                      * on hip_stream before it; the front ends of the later calls of the run
+                                      * wait only for the earlier frames of their workspaces (on the device),
+                                      * so inputs (Gaussians, ids, chunk bounds) written on the stream during a
+                                      * run must be followed by one call without this flag — like a Vulkan frame
+                                      * in flight, whose resources the application does not touch. Same image,
+                                      * keys and counts as without the flag. */
 int ptgs_set_flags(ptgs_ctx* ctx, uint32_t flags);
 int ptgs_stats_reset(ptgs_ctx* ctx, void* hip_stream);
 int ptgs_stats_read(ptgs_ctx* ctx, ptgs_trace_stats* out); /* synchronises the context's device */

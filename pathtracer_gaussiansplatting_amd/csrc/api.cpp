@@ -57,15 +57,21 @@ struct ptgs_ctx {
   hipStream_t view_stream[PTGS_MAX_VIEWS] = {};
   hipEvent_t view_fork = nullptr, view_join[PTGS_MAX_VIEWS] = {};
   // PTGS_FLAG_SPLAT_OVERLAP: a ring of workspaces (`splat` is always the latest call's; ov_ring[0] is the
-  // context's own first workspace), the front-end stream, the caller's stream at the start of every
-  // (depth - 1)-th call (ov_call[0] / [1] alternately; see splat_overlap_begin), the front end's end
+  // context's own first workspace), the front-end stream, the caller's stream at the start of a run of
+  // overlapped calls (ov_call[0]; see splat_overlap_begin), the front end's end
   SplatWorkspace* ov_ring[PTGS_OV_RING] = {};
   hipStream_t ov_stream = nullptr;
-  hipEvent_t ov_call[2] = {}, ov_done = nullptr;
+  hipEvent_t ov_call[1] = {}, ov_done = nullptr;
   uint32_t ov_pos = 0;      // ring slot of the latest overlapped call
   uint32_t ov_depth = 0;    // workspaces in use (2 .. PTGS_OV_RING)
   uint32_t pending_report = 0;  // earlier frames' reports a failing splat call collected (returned by the next)
-  uint32_t ov_started = 0;  // consecutive overlapped calls so far (0: the next one records and waits for its own marker)
+  uint32_t ov_started = 0;  // consecutive overlapped calls so far (0: the next one starts a run from the caller's stream)
+  // blend ordinals (SplatSeq): the device word the blends store theirs in, the next one, and per call of the
+  // run (k % 4) the ordinal of its blend (0: none launched) and its stream
+  unsigned long long* ov_flag = nullptr;
+  unsigned long long ov_next = 1;
+  unsigned long long ov_ord[4] = {};
+  hipStream_t ov_strm[4] = {};
   ptgs::WfWorkspace wf;  // wavefront path tracer buffers (PTGS_FLAG_PT_WAVEFRONT)
   ptgs::PtSched pt_sched;  // megakernel tile schedule (heavy tiles first)
   void* comm = nullptr;  // RCCL communicator (ptgs_comm_create)
@@ -225,6 +231,7 @@ void ptgs_destroy(ptgs_ctx* c) {
   for (hipEvent_t ev : c->ov_call)
     if (ev) (void)hipEventDestroy(ev);
   if (c->ov_done) (void)hipEventDestroy(c->ov_done);
+  if (c->ov_flag) (void)hipFree(c->ov_flag);
   if (c->comm) (void)comm_destroy(c->comm);
   delete c;
 }
@@ -703,7 +710,7 @@ extern "C" {
 static int splat_render(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
                         const float bg[3], const float* depth, const float* under, uint32_t tile_row_begin,
                         uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream, uint32_t* report,
-                        const SplatOverlap* ov = nullptr) {
+                        const SplatOverlap* ov = nullptr, SplatSeq* seq = nullptr) {
   *report = 0;
   if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(c, PTGS_EINVAL, "bad image size %ux%u", w, h);
   if (g->count && (!is_device_ptr(g->means) || !is_device_ptr(g->scales) || !is_device_ptr(g->rotations) ||
@@ -719,7 +726,7 @@ static int splat_render(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
   hipError_t e = splat_gaussians(c->splat, g, ubo->view, mvp, ubo->proj[0], ubo->proj[5], w, h, bg, depth, under,
                                  tile_row_begin, tile_row_end, out, stats, (c->flags & PTGS_FLAG_TIME_STAGES) != 0,
                                  (c->flags & PTGS_FLAG_SPLAT_PUBLISH) != 0, (c->flags & PTGS_FLAG_SPLAT_PUBLISH_TIGHT) != 0,
-                                 (hipStream_t)stream, report, ov);
+                                 (hipStream_t)stream, report, ov, seq);
   if (e != hipSuccess) return fail(c, PTGS_EHIP, "splat_gaussians: %s", hipGetErrorString(e));
   return PTGS_OK;
 }
@@ -746,11 +753,10 @@ static int splat_report(ptgs_ctx* c, uint32_t report) {
 }
 
 // PTGS_FLAG_SPLAT_OVERLAP: the call takes the ring's next workspace (the one of the call depth calls back)
-// and, for a stream-ordered frame, its front end runs on the context's second stream once the caller's
-// stream has finished what it held at the start of one of the last depth - 1 calls: that covers the
-// workspace's last frame (blend included) and the inputs the caller wrote before then. Without the flag
-// the front end follows the caller's stream (ov_started is cleared: the next overlapped call starts
-// from the caller's stream as it is then).
+// and, for a stream-ordered frame, its front end runs on the context's second stream. The first call of a
+// run of overlapped calls starts it after everything the caller's stream holds; later calls' front ends
+// wait on the device for the earlier blends of their workspace only (gs_done_wait), so inputs the caller
+// writes during a run are not seen by it. A call without the flag ends the run (ov_started is cleared).
 // workspaces in the ring, fixed when a context first overlaps (PTGS_GS_OV_DEPTH=2 .. 4; A/B switch)
 static uint32_t overlap_depth() {
   const char* v = getenv("PTGS_GS_OV_DEPTH");
@@ -758,7 +764,7 @@ static uint32_t overlap_depth() {
   return (uint32_t)std::max(2, std::min(x, PTGS_OV_RING));
 }
 
-static int splat_overlap_begin(ptgs_ctx* c, hipStream_t s, SplatOverlap* ov) {
+static int splat_overlap_begin(ptgs_ctx* c, hipStream_t s, SplatOverlap* ov, SplatSeq* seq) {
   HIPCHK(c, hipSetDevice(c->device));
   if (!c->ov_ring[0]) {  // the ring starts at the current workspace
     c->ov_ring[0] = c->splat;
@@ -783,23 +789,43 @@ static int splat_overlap_begin(ptgs_ctx* c, hipStream_t s, SplatOverlap* ov) {
     const char* v = getenv("PTGS_GS_OV_FENCE");
     return (unsigned)(hipEventDisableTiming | (v && !strcmp(v, "1") ? 0u : (unsigned)hipEventDisableSystemFence));
   }();
-  for (hipEvent_t* ev : {&c->ov_call[0], &c->ov_call[1], &c->ov_done})
+  for (hipEvent_t* ev : {&c->ov_call[0], &c->ov_done})
     if (!*ev) HIPCHK(c, hipEventCreateWithFlags(ev, ev_flags));
-  // the next ring slot; the workspace there was last used depth calls ago. The front end waits for a
-  // marker of the caller's stream recorded at the start of one of the last depth - 1 calls (the caller's
-  // stream had finished the workspace's last frame there, blend included). Markers are recorded every
-  // depth - 1 calls only (into two alternating events): a marker beside the cross-queue barrier costs the
-  // caller's queue ~3 us per frame (tools/micro/queue_sync.hip: wait + marker 28.0 vs wait alone 25.1 us on a
-  // 22 us kernel), so the front end of call k waits for the marker of call m (k - 1) / m, m = depth - 1
-  // (call 0: its own), and sees the caller's work enqueued before the call depth - 1 calls back.
+  if (!c->ov_flag) {  // (signal memory for the front end's wait-value packet; zero before any blend stores)
+    HIPCHK(c, hipExtMallocWithFlags((void**)&c->ov_flag, 8, hipMallocSignalMemory));
+    HIPCHK(c, hipMemset(c->ov_flag, 0, 8));
+  }
+  // the next ring slot; the workspace there was last used depth calls ago (call k - depth). Its blend ran
+  // before the blend of call k - depth + 1 on the caller's stream, so once THAT blend has started (its
+  // ordinal in ov_flag, SplatSeq) the workspace is free: the front end's queue waits for that value and the
+  // caller's queue carries no marker (a marker beside the cross-queue barrier had cost it ~3-5 us per frame:
+  // tools/micro/queue_sync.hip, wait + marker 28.0 vs wait alone 25.1 us on a 22 us kernel; kernel trace
+  // 10.5 vs 6.0 us between two blends). The first call of a run waits for a marker of the caller's stream
+  // (everything enqueued before the run), as do calls whose ordering is not known (no blend launched, or a
+  // call on another stream: then a new marker).
   const uint32_t cur = (c->ov_pos + 1) % depth;
   c->ov_pos = cur;
   c->splat = c->ov_ring[cur];
-  const uint32_t m = depth - 1, k = c->ov_started;
-  if (k % m == 0) HIPCHK(c, hipEventRecord(c->ov_call[(k / m) & 1u], s));
+  const uint32_t k = c->ov_started, back = depth - 1;
+  bool same = true;
+  for (uint32_t j = 1; j <= std::min(k, back); ++j) same = same && c->ov_strm[(k - j) & 3u] == s;
   ov->fe = c->ov_stream;
-  ov->wait = c->ov_call[k == 0 ? 0u : ((k - 1) / m) & 1u];
   ov->done = c->ov_done;
+  ov->wait = nullptr;
+  ov->wait_flag = nullptr;
+  ov->wait_ordinal = 0;
+  if (k >= back && same && c->ov_ord[(k - back) & 3u]) {
+    ov->wait_flag = c->ov_flag;
+    ov->wait_ordinal = c->ov_ord[(k - back) & 3u];
+  } else {
+    // (k < back on the run's stream: the workspace was last used before the run, so the marker recorded at
+    // the run's start (or a later one) covers it; otherwise a new marker)
+    if (!(k > 0 && k < back && same)) HIPCHK(c, hipEventRecord(c->ov_call[0], s));
+    ov->wait = c->ov_call[0];
+  }
+  seq->flag = c->ov_flag;
+  seq->ordinal = c->ov_next;
+  seq->launched = false;
   // the blend's tile order: the front end's order workgroup from the workspace's previous frame (default),
   // or PTGS_GS_OV_ORDER=own: a launch behind the front end from the frame's own counts (A/B switch;
   // measured slower at C2 static, 0.0531 vs 0.0521 ms, and not faster on the orbit: DESIGN §5 round 6)
@@ -808,8 +834,16 @@ static int splat_overlap_begin(ptgs_ctx* c, hipStream_t s, SplatOverlap* ov) {
     return v && !strcmp(v, "own");
   }();
   ov->own_order = own_order;
-  c->ov_started = k + 1u;  // (wraps to 0 after 2^32 calls: a call that waits for its own marker, safe)
   return PTGS_OK;
+}
+
+// after the call's frame: its blend's ordinal and stream (see splat_overlap_begin)
+static void splat_overlap_end(ptgs_ctx* c, hipStream_t s, const SplatSeq& seq) {
+  const uint32_t k = c->ov_started;
+  c->ov_ord[k & 3u] = seq.launched ? seq.ordinal : 0u;
+  c->ov_strm[k & 3u] = s;
+  if (seq.launched) c->ov_next = seq.ordinal + 1u;
+  c->ov_started = k + 1u < 4u ? k + 1u : 4u + ((k + 1u) & 3u);  // (>= 4: every look-back valid; the index mod 4 kept)
 }
 
 static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ubo, uint32_t w, uint32_t h,
@@ -817,16 +851,18 @@ static int splat_common(ptgs_ctx* c, const ptgs_gaussians* g, const ptgs_ubo* ub
                         uint32_t tile_row_end, float* out, ptgs_splat_stats* stats, void* stream) {
   uint32_t report = 0;
   SplatOverlap ov{};
+  SplatSeq seq{};
   const SplatOverlap* ovp = nullptr;
   if (c->flags & PTGS_FLAG_SPLAT_OVERLAP) {
-    const int rc = splat_overlap_begin(c, (hipStream_t)stream, &ov);
+    const int rc = splat_overlap_begin(c, (hipStream_t)stream, &ov, &seq);
     if (rc != PTGS_OK) return rc;
     ovp = &ov;  // (splat_gaussians runs a frame with stats / publish / stage timing serially anyway)
   } else {
     c->ov_started = 0;
   }
   const int rc = splat_render(c, g, ubo, w, h, bg, depth, under, tile_row_begin, tile_row_end, out, stats, stream,
-                              &report, ovp);
+                              &report, ovp, ovp ? &seq : nullptr);
+  if (ovp) splat_overlap_end(c, (hipStream_t)stream, seq);
   return splat_finish(c, rc, report);
 }
 

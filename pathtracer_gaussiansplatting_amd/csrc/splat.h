@@ -14,12 +14,25 @@ void splat_workspace_destroy(SplatWorkspace* w);
 
 // Front end on a second stream (PTGS_FLAG_SPLAT_OVERLAP, fused frames): the front end (and, with
 // own_order, the blend's tile order from this frame's own pair counts) runs on `fe` once `wait` has
-// completed; `done` is recorded behind it and the caller's stream waits for it before the blend. So the
-// front end of frame k overlaps the blend of frame k - 1 (another workspace) on the caller's stream.
+// completed, or (wait null) once the word wait_flag holds at least wait_ordinal (a stream wait-value packet:
+// the blend after the workspace's last one has started, SplatSeq); `done` is recorded behind it and the
+// caller's stream waits for it before the blend. So the front end of frame k overlaps the blend of frame
+// k - 1 (another workspace) on the caller's stream.
 struct SplatOverlap {
   hipStream_t fe;
   hipEvent_t wait, done;
+  unsigned long long* wait_flag;
+  unsigned long long wait_ordinal;
   bool own_order;
+};
+// The blend ordinals of a context that overlaps frames: the first workgroup of the blend of this call stores
+// `ordinal` in *flag (signal memory) when it starts. Blends run in the caller's stream's order, each kernel
+// after the previous one has ended (its kernel-end cache write-back included), so ordinal n in the flag means
+// every earlier blend has finished. `launched` is set when a blend was launched with it.
+struct SplatSeq {
+  unsigned long long* flag;
+  unsigned long long ordinal;
+  bool launched;
 };
 
 // view/mvp column-major float[16]; p00 = proj[0][0], p11 = proj[1][1] (negative: Vulkan y-down)
@@ -30,7 +43,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
                            ptgs_splat_stats* stats, bool time_stages, bool publish, bool publish_tight, hipStream_t s,
                            uint32_t* report,  // report: bit 0 an earlier frame was left incomplete, bit 1 ids >= N
-                           const SplatOverlap* ov = nullptr);
+                           const SplatOverlap* ov = nullptr, SplatSeq* seq = nullptr);
 hipError_t splat_stage_ms(SplatWorkspace* w, float* out_ms);
 // 3D Morton order of the means: a reordered copy + the original indices (synchronises s)
 hipError_t splat_sort_spatial(const ptgs_gaussians* g, float* means, float* scales, float* rots, float* opac,

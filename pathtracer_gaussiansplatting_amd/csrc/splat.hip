@@ -1084,6 +1084,8 @@ struct GsFused {  // the sort's and the blend's view of a fused-front-end frame 
   const uint32_t* order;  // blend workgroup -> tile (heavy tiles first; null: row-major)
   uint2* fsq;             // the front end's slice queue (re-armed by block (0, 0): entries and fz[12..14])
   uint32_t fsq_cap;
+  unsigned long long* seq_flag;  // frames in flight: the blend's first workgroup stores `seq` here (SplatSeq)
+  unsigned long long seq;
 };
 // Work-items per fused workgroup (GS_FUSED_THREADS Gaussians; all walk the pairs): 512 for a frame on the
 // caller's stream; 256 for an overlapped frame (SplatOverlap), whose front end runs beside the previous
@@ -2023,6 +2025,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   __shared__ uint8_t s_sslot[GS_BLOCK];  // small tiles: staging slot of sorted position p
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   STAMP(1, 0);
+  if (fu.seq_flag && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)  // (this blend has started: SplatSeq)
+    __hip_atomic_store(fu.seq_flag, fu.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (fu.scap) {
     // fused front end: block (0, 0) hands the frame's counters to the host and re-arms them (the
     // fused kernel that produced them has finished; no other blend block reads them)
@@ -2453,7 +2457,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                            float p11, uint32_t W, uint32_t H, const float bg[3], const float* depth,
                            const float* under, uint32_t tile_row_begin, uint32_t tile_row_end, float* out,
                            ptgs_splat_stats* stats, bool time_stages, bool publish, bool publish_tight, hipStream_t s,
-                           uint32_t* report, const SplatOverlap* ov) {
+                           uint32_t* report, const SplatOverlap* ov, SplatSeq* seq) {
   hipError_t e;
   *report = 0;
   if (stats || publish || time_stages) ov = nullptr;  // (these frames are synchronous or instrumented: serial)
@@ -2712,7 +2716,9 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
                        (const float4*)w->rec.p, bg[0], bg[1], bg[2], cap, slot_keys,
                        (const unsigned long long*)w->tile_slots.p, depth, (const float4*)under, (float4*)out, fu,
                        spill_args(fu.scap != 0));
-    return hipGetLastError();
+    const hipError_t le = hipGetLastError();
+    if (!le && seq && fu.seq_flag) seq->launched = true;
+    return le;
   };
   auto sort_attr = [&]() -> hipError_t {
     if (w->sort_attr) return hipSuccess;
@@ -2728,7 +2734,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if ((e = ensure(w->order, (size_t)tiles * 4))) return e;
     order = (uint32_t*)w->order.p;
   }
-  const GsFused no_fu = {0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order, nullptr, 0u};
+  const GsFused no_fu = {0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, order, nullptr, 0u,
+                         seq ? seq->flag : nullptr, seq ? seq->ordinal : 0ull};
 
   auto enqueue_fused = [&]() -> hipError_t {
     hipError_t e2;
@@ -2737,7 +2744,12 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     if (publish && (e2 = ensure(w->keys_out, (size_t)tiles * scap * 8))) return e2;
     // the front end's stream: the caller's, or (overlapped frame) the second stream once ov->wait is done
     const hipStream_t sf = ov ? ov->fe : s;
-    if (ov && (e2 = hipStreamWaitEvent(sf, ov->wait, 0))) return e2;
+    if (ov && ov->wait && (e2 = hipStreamWaitEvent(sf, ov->wait, 0))) return e2;
+    // (or the workspace's reuse from the blend ordinals, SplatSeq: a wait packet on the front end's queue,
+    // which holds no workgroup slots while it waits and puts nothing on the caller's queue)
+    if (ov && ov->wait_flag &&
+        (e2 = hipStreamWaitValue64(sf, (void*)ov->wait_flag, ov->wait_ordinal, hipStreamWaitValueGte, ~0ull)))
+      return e2;
     if (w->cursor.bytes < (size_t)tiles * 4) {  // zero between frames (the blend re-arms what it reads)
       if ((e2 = ensure(w->cursor, (size_t)tiles * 4))) return e2;
       if ((e2 = hipMemsetAsync(w->cursor.p, 0, w->cursor.bytes, sf))) return e2;
@@ -2765,7 +2777,8 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     }
     const uint32_t fsq_cap = (uint32_t)std::min<size_t>(w->fsq.bytes / 8, 0x7FFFFFFFu);
     GsFused fu = {scap, (uint32_t*)w->cursor.p, (uint32_t*)w->fz.p, w->k_dev, (uint2*)w->ranges.p,
-                  (uint32_t*)w->fzp.p, nwg, order, (uint2*)w->fsq.p, fsq_cap};
+                  (uint32_t*)w->fzp.p, nwg, order, (uint2*)w->fsq.p, fsq_cap, seq ? seq->flag : nullptr,
+                  seq ? seq->ordinal : 0ull};
     PreArgs fpa = pa;  // the fused walk keeps rects / depths in registers (band 0 stores them for gs_spill_tile)
     if (cam.cull && (n + 255u) / 256u > GS_FUSED_OWN_CULL) {
       if ((e2 = cull_flags(sf))) return e2;
