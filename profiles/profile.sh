@@ -18,8 +18,11 @@ sha256sum pathtracer_gaussiansplatting_amd/libptgs.so > "$OUT/lib_sha256.txt"  #
 export TMPDIR=/tmp
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_kt.log" 2>&1
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_fetch.log" 2>&1
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_write.log" 2>&1
-timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/tcc" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_tcc.log" 2>&1
-timeout -k 10 600 rocprofv3 --pmc $SQ -d "$OUT/sq" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_sq.log" 2>&1
+# (counter passes with one frame at a time: under --pmc the front end's stream wait-value packet behind
+# the serialised dispatches stalled the frames-in-flight loop (r06); the blend is the same kernel either way)
+PARGS="$ARGS --no-splat-overlap"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 bench.py $PARGS > "$OUT/bench_fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 bench.py $PARGS > "$OUT/bench_write.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/tcc" -o run --output-format csv -- python3 bench.py $PARGS > "$OUT/bench_tcc.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc $SQ -d "$OUT/sq" -o run --output-format csv -- python3 bench.py $PARGS > "$OUT/bench_sq.log" 2>&1
 echo "profiles collected in $OUT"
