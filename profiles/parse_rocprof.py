@@ -115,6 +115,7 @@ def main(tag, workload):
                                        "fetch_kib": fa, "write_kib": wa, "hbm_bytes_per_launch": hbm,
                                        "hbm_gbs": gbs, "l2_hit": l2, "valu_lane_util": lanes,
                                        "valu_issue_share": issue, "wave_wait_share": wait}
+    lines += _two_queue_timeline(base)
     with open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w") as fh:
         fh.write("\n".join(lines) + "\n")
     out = _finite(out)
@@ -122,6 +123,29 @@ def main(tag, workload):
         json.dump(out, fh, indent=1)
     print("\n".join(lines))
     print(json.dumps(out, indent=1))
+
+
+def _two_queue_timeline(base, count=16):
+    """The 3DGS dispatches of the kernel trace on a timeline (frames in flight put the front end and the
+    blend on two queues): 16 consecutive ones from 60% into the trace, times relative to the first."""
+    import csv
+    import glob
+    f = sorted(glob.glob(os.path.join(base, "kt", "*kernel_trace.csv")))
+    if not f:
+        return []
+    rows = sorted((r for r in csv.DictReader(open(f[0])) if "gs_bin_fused" in r["Kernel_Name"] or
+                   "gs_sort_blend" in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
+    if len({r["Queue_Id"] for r in rows}) < 2:
+        return []
+    sub = rows[int(len(rows) * 0.6):][:count]
+    t0 = int(sub[0]["Start_Timestamp"])
+    out = ["", "## two-queue timeline (frames in flight: front end and blend of consecutive frames)", "",
+           "| start us | end us | dur us | queue | kernel |", "|---|---|---|---|---|"]
+    for r in sub:
+        a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("ptgs::", "")
+        out.append(f"| {(a - t0) / 1e3:.1f} | {(b - t0) / 1e3:.1f} | {(b - a) / 1e3:.1f} | {r['Queue_Id']} | {name} |")
+    return out
 
 
 def _div(a, b):
