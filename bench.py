@@ -67,9 +67,10 @@ def parse():
     return ap.parse_args()
 
 
-def _profiled(kernel: str):
+def _profiled(kernel: str, need_traffic: bool = True):
     """rocprof figures of `kernel` from profiles/traffic_latest.json, only if they were collected on this
-    exact libptgs.so (sha256) — otherwise None (the numbers would describe another build)."""
+    exact libptgs.so (sha256) — otherwise None (the numbers would describe another build). need_traffic:
+    only an entry the counter passes saw (HBM bytes per launch); else the kernel trace's duration suffices."""
     import hashlib
     tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
     try:
@@ -79,7 +80,7 @@ def _profiled(kernel: str):
         if tj.get("lib_sha256") != lib_sha:
             return None
         e = tj.get("kernels", {}).get(kernel)
-        return e if e and e.get("hbm_bytes_per_launch") else None
+        return e if e and (e.get("hbm_bytes_per_launch") or (not need_traffic and e.get("avg_ms"))) else None
     except (OSError, ValueError):
         return None
 
@@ -625,9 +626,9 @@ def main():
             # else per-stage HIP events of an untimed serial pass (each event pair adds its launch gap: the stages
             # sum past ms_per_step, which is the timed frame)
             "stages_us_kernel_trace": {k: round(float(e["avg_ms"]) * 1e3, 2) for k, e in
-                                       (("front_end_overlapped", _profiled("gs_bin_fused_kernel_ov")),
-                                        ("front_end_serial", _profiled("gs_bin_fused_kernel")),
-                                        ("sort_blend", _profiled("gs_sort_blend_kernel"))) if e} or None,
+                                       (("front_end_overlapped", _profiled("gs_bin_fused_kernel_ov", False)),
+                                        ("front_end_serial", _profiled("gs_bin_fused_kernel", False)),
+                                        ("sort_blend", _profiled("gs_sort_blend_kernel", False))) if e} or None,
             "stages_ms_event_timed": {k: round(float(v), 4) for k, v in
                           zip(["front_end" if gstat.fused else "preprocess+count", "colscan", "scatter", "sort_large",
                                "-", "sort_blend"], stages) if k != "-" and not (gstat.fused and k in ("colscan", "scatter"))},
