@@ -521,3 +521,48 @@ def test_gaussians_overlap_mixed_calls(native_lib, oracle_lib):
     finally:
         ra.close()
         rb.close()
+
+
+def test_gaussians_overlap_runs_and_streams(native_lib):
+    """The run rule of PTGS_FLAG_SPLAT_OVERLAP (ptgs.h): within a run the front ends wait on the device for
+    the blend ordinals only; a call without the flag ends the run, so Gaussians rewritten on the stream
+    before it are seen by the next run; calls that switch streams mid-run fall back to a marker of the new
+    stream. Every image equals the serial render of the Gaussians it was called with, bit for bit."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H, n = 480, 270, 20_000
+    g = Y.gaussians_c2(n, seed=35)
+    g2 = dict(g, colors=(1.0 - g["colors"]).astype(np.float32))  # (the rewritten set: other colours)
+    ubos = [orbit_ubo(k, W, H) for k in range(12)]
+    ra, rb = Renderer(0), Renderer(0)
+    try:
+        ra.set_splat_overlap(True)
+        da = {k: _dev(v) for k, v in g.items()}
+        ref1 = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in ubos]
+        ref2 = [torch.zeros_like(o) for o in ref1]
+        db1, db2 = {k: _dev(v) for k, v in g.items()}, {k: _dev(v) for k, v in g2.items()}
+        for u, o1, o2 in zip(ubos, ref1, ref2):
+            rb.splat_gaussians(db1, u, W, H, o1)
+            rb.splat_gaussians(db2, u, W, H, o2)
+        out = [torch.zeros_like(o) for o in ref1]
+        for k in range(5):  # a run on the current stream
+            ra.splat_gaussians(da, ubos[k], W, H, out[k])
+        # the colours rewritten on the stream, then one call without the flag ends the run
+        da["colors"].copy_(torch.from_numpy(g2["colors"]).cuda())
+        ra.set_splat_overlap(False)
+        ra.splat_gaussians(da, ubos[5], W, H, out[5])
+        ra.set_splat_overlap(True)
+        side = torch.cuda.Stream()
+        for k in range(6, 12):  # a new run; calls 8 and 10 on a side stream (ordered after the others)
+            if k in (8, 10):
+                side.wait_stream(torch.cuda.current_stream())
+                ra.splat_gaussians(da, ubos[k], W, H, out[k], stream=side)
+                torch.cuda.current_stream().wait_stream(side)
+            else:
+                ra.splat_gaussians(da, ubos[k], W, H, out[k])
+        torch.cuda.synchronize()
+        assert ra.splat_status().frames == 0
+        diff = [k for k in range(12) if not torch.equal(out[k], (ref1 if k < 5 else ref2)[k])]
+        assert not diff, diff
+    finally:
+        ra.close()
+        rb.close()
