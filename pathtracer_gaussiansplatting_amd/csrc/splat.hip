@@ -2187,12 +2187,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     const uint32_t m = (n + 63u) >> 6;  // runs holding keys (uniform)
     unsigned long long sk = ~0ull;
     if (wave < m) {
-      sk = gs_wave_sort64(key, lane);
+      sk = GS_PROBE(GS_PROBE_NO_MERGE) ? key : gs_wave_sort64(key, lane);
       s_key[tid] = sk;
     }
     __syncthreads();
-    uint32_t r = lane;
-    if (wave < m) r += gs_runs_below<GS_BLOCK / 64>(s_key, m, wave, sk);
+    uint32_t r = GS_PROBE(GS_PROBE_NO_MERGE) ? tid : lane;
+    if (wave < m && !GS_PROBE(GS_PROBE_NO_MERGE)) r += gs_runs_below<GS_BLOCK / 64>(s_key, m, wave, sk);
     __syncthreads();  // every read of the keys is done before records overwrite them
     if (tid < n) s_mask[tid] = (uint8_t)stage_rec(tid, ra, rb, rc, !GS_PROBE(GS_PROBE_NO_EXACT));
     if (sk != ~0ull) {

@@ -14,6 +14,7 @@
 #define GS_PROBE_NO_REC 2u   // small tiles skip the record gather (its latency)
 #define GS_PROBE_NO_RANK 4u  // small tiles rank by identity (the sort's cost)
 #define GS_PROBE_NO_EXACT 8u  // small tiles stage with the alpha-box quadrant test only (same image: both are conservative)
+#define GS_PROBE_NO_MERGE 16u  // small tiles above GS_MERGE_MIN rank by identity (the wave sort + run searches' cost)
 #define GS_PROBE(bit) ((GS_PROBES & (bit)) != 0u)
 
 #ifdef GS_STAMP
