@@ -501,12 +501,12 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t x, uint32_t lane) {
     const int t = __builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // row_mirror
     return (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x141, 0xF, 0xF, false);    // row_half_mirror
   }
-  if (J == 16) {  // odd rows of the first result, even rows of the second
+  if (J == 16) {  // odd rows of the first result, even rows of the second (the rows as a constant lane mask)
     const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    return ((lane >> 4) & 1u) ? r[0] : r[1];
+    return __builtin_amdgcn_inverse_ballot_w64(0xFFFF0000FFFF0000ull) ? r[0] : r[1];
   }
   const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // J == 32
-  return lane >= 32u ? r[0] : r[1];
+  return __builtin_amdgcn_inverse_ballot_w64(0xFFFFFFFF00000000ull) ? r[0] : r[1];
 }
 template <uint32_t J>
 __device__ __forceinline__ unsigned long long lane_xor64(unsigned long long x, uint32_t lane) {
@@ -1802,11 +1802,24 @@ __global__ __launch_bounds__(GS_SORT_THREADS) void gs_sort_large_kernel(
 // ~200 VALU per key for 2-4 runs and ~400 for 8 instead of n / 4 compares against every key (the
 // counting below): keys are unique, so the ranks are the same.
 // (the exchanges through DPP and the gfx950 permlane swaps: no LDS round trip per step)
+// the lanes of a bitonic step (K, J) that keep the smaller key: ascending blocks' low halves and descending
+// blocks' high halves (a compile-time lane mask)
+template <uint32_t K, uint32_t J>
+__host__ __device__ constexpr unsigned long long gs_keep_min_mask() {
+  unsigned long long m = 0;
+  for (uint32_t l = 0; l < 64u; ++l)
+    if (((l & K) == 0u) == ((l & J) == 0u)) m |= 1ull << l;
+  return m;
+}
+// one compare-exchange step: a lane takes its partner's key iff (partner < own) equals "keeps the
+// minimum" — one 64-bit compare, the lane mask applied to its result in SGPRs, two selects (the min / max
+// form compared twice and selected three times: 21 steps x ~6 VALU more per wave sort, ~0.7 M VALU per
+// C2 frame)
 template <uint32_t K, uint32_t J>
 __device__ __forceinline__ unsigned long long gs_sort_step(unsigned long long x, uint32_t lane) {
   const unsigned long long y = lane_xor64<J>(x, lane);
-  const bool asc = (lane & K) == 0u, low = (lane & J) == 0u;
-  return (asc == low) ? (y < x ? y : x) : (y < x ? x : y);
+  const unsigned long long take = ~(__builtin_amdgcn_ballot_w64(y < x) ^ gs_keep_min_mask<K, J>());
+  return __builtin_amdgcn_inverse_ballot_w64(take) ? y : x;
 }
 __device__ __forceinline__ unsigned long long gs_wave_sort64(unsigned long long x, uint32_t lane) {
   x = gs_sort_step<2, 1>(x, lane);
