@@ -127,7 +127,8 @@ def main(tag, workload):
 
 def _two_queue_timeline(base, count=16):
     """The 3DGS dispatches of the kernel trace on a timeline (frames in flight put the front end and the
-    blend on two queues): 16 consecutive ones from 60% into the trace, times relative to the first."""
+    blend on two queues): the first 16 consecutive ones from 40% into the trace that show both queues in a
+    steady state (blends within 15 us of each other), times relative to the first."""
     import csv
     import glob
     f = sorted(glob.glob(os.path.join(base, "kt", "*kernel_trace.csv")))
@@ -137,7 +138,13 @@ def _two_queue_timeline(base, count=16):
                    "gs_sort_blend" in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
     if len({r["Queue_Id"] for r in rows}) < 2:
         return []
-    sub = rows[int(len(rows) * 0.6):][:count]
+    def steady(w):  # both queues, and every blend within 15 us of the previous blend's end
+        bl = [r for r in w if "gs_sort_blend" in r["Kernel_Name"]]
+        gaps = [int(b["Start_Timestamp"]) - int(a["End_Timestamp"]) for a, b in zip(bl, bl[1:])]
+        return len({r["Queue_Id"] for r in w}) > 1 and len(bl) > 3 and max(gaps) < 15000
+    start = next((i for i in range(int(len(rows) * 0.4), len(rows) - count) if steady(rows[i:i + count])),
+                 int(len(rows) * 0.6))
+    sub = rows[start:start + count]
     t0 = int(sub[0]["Start_Timestamp"])
     out = ["", "## two-queue timeline (frames in flight: front end and blend of consecutive frames)", "",
            "| start us | end us | dur us | queue | kernel |", "|---|---|---|---|---|"]
