@@ -55,7 +55,31 @@ def rebalance_tile_rows(split, band_ms, row_pairs, tiles_x: int, tile_cost: floa
     for (a, b), ms in zip(split, band_ms):
         if b > a:
             cost[a:b] = float(ms) * w[a:b] / max(w[a:b].sum(), 1e-30)
-    return _split_rows(cost, len(split))
+    return _refine_split(_split_rows(cost, len(split)), cost)
+
+
+def _refine_split(split, cost, iters: int = 64) -> list[tuple[int, int]]:
+    """Lower the costliest band of a contiguous split by moving its edge row to a neighbour while that lowers
+    the larger of the two (the equal-share cut places each boundary independently; with rows of ~0.14 ms at
+    the 10M / 4K frame's centre it left a band one row above its neighbours, r06e: 1.435 vs 1.276 ms)."""
+    import numpy as np
+    c = np.concatenate([[0.0], np.cumsum(np.asarray(cost, np.float64))])
+    b = [s for s, _ in split] + [split[-1][1]]
+    band = lambda i: c[b[i + 1]] - c[b[i]]
+    for _ in range(iters):
+        i = max(range(len(split)), key=band)
+        best = None
+        if i > 0 and b[i + 1] - b[i] > 1:  # its first row to the band before
+            m = max(c[b[i] + 1] - c[b[i - 1]], c[b[i + 1]] - c[b[i] + 1])
+            best = (m, i, +1)
+        if i + 1 < len(split) and b[i + 1] - b[i] > 1:  # its last row to the band after
+            m = max(c[b[i + 1] - 1] - c[b[i]], c[b[i + 2]] - c[b[i + 1] - 1])
+            if best is None or m < best[0]:
+                best = (m, i + 1, -1)
+        if best is None or best[0] >= band(i) - 1e-12:
+            break
+        b[best[1]] += best[2]
+    return [(b[i], b[i + 1]) for i in range(len(split))]
 
 
 def _split_rows(w, world: int) -> list[tuple[int, int]]:

@@ -485,3 +485,25 @@ def test_rebalance_tile_rows():
     cost = np.where(np.arange(40) < 10, 0.2, 0.1)
     per = [cost[a:b].sum() for a, b in new]
     assert max(per) - min(per) <= 0.2 + 1e-9, per
+
+
+def test_refine_split_lowers_the_costliest_band():
+    """dist._refine_split (the feedback re-split's last step): the result still covers every row once, in
+    order, with the same number of bands, and its costliest band is never above the equal-share cut's; on
+    a split that left a band one heavy row above its neighbour it moves that row over."""
+    from pathtracer_gaussiansplatting_amd import dist as D
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        n, world = int(rng.integers(4, 40)), int(rng.integers(2, 6))
+        cost = rng.uniform(0.05, 1.0, n) ** 3
+        base = D._split_rows(cost, world)
+        ref = D._refine_split(base, cost)
+        assert len(ref) == world and ref[0][0] == 0 and ref[-1][1] == n
+        assert all(a[1] == b[0] and a[0] <= a[1] for a, b in zip(ref, ref[1:]))
+        band_max = lambda sp: max(cost[a:b].sum() for a, b in sp)
+        assert band_max(ref) <= band_max(base) + 1e-12
+    cost = np.array([1.0, 1.0, 1.0, 1.0, 3.0, 3.0, 1.0, 1.0])
+    split = [(0, 5), (5, 8)]  # 7 vs 5: moving the heavy row over would give 4 vs 8, so it stays
+    assert D._refine_split(split, cost) == [(0, 5), (5, 8)]
+    split = [(0, 6), (6, 8)]  # 10 vs 2: the heavy row moves -> 7 vs 5
+    assert D._refine_split(split, cost) == [(0, 5), (5, 8)]

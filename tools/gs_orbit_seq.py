@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The gs_orbit leg in the order bench.py runs it (after the static C2 loop, the views4 leg and the generated-
-order frames) against right after the static loop, frames in flight and serial, GS_REPS times each, one
-process: does what ran before change the overlapped orbit?   tools/gs_orbit_seq.py"""
+order frames, the stats frame and the per-stage event pass: GS_STATS / GS_STAGES=0 leave them out) against
+right after the static loop, frames in flight and serial, GS_REPS times each, one process: does what ran
+before change the overlapped orbit?   tools/gs_orbit_seq.py"""
 import os
 import sys
 import time
@@ -44,6 +45,16 @@ def main():
         torch.cuda.synchronize()
 
     def other_legs():
+        from pathtracer_gaussiansplatting_amd import FLAG_TIME_STAGES
+        r.set_splat_overlap(False)
+        if os.environ.get("GS_STATS", "1") == "1":  # the bench's stats frame (3-sigma rectangles, K read back)
+            r.splat_gaussians(dg, ubo, W, H, img, want_stats=True)
+        if os.environ.get("GS_STAGES", "1") == "1":  # the bench's per-stage event pass
+            r.set_flags(FLAG_TIME_STAGES)
+            for _ in range(100):
+                r.splat_gaussians(dg, ubo, W, H, img)
+                r.splat_stage_ms()
+            r.set_flags(0)
         vubos = [make_ubo(Camera(aspect=W / H).look_at([0.25 * k, 0.0, 0.0], [0.25 * k, 0.0, -1.0]),
                           cornell_box_scene(), 0) for k in range(4)]
         vouts = [torch.zeros_like(img) for _ in vubos]
@@ -54,10 +65,10 @@ def main():
             r.splat_gaussians(dg0, ubo, W, H, img)
         torch.cuda.synchronize()
 
-    for order in ("after the static loop", "after views4 + generated order"):
+    for order in ("after the static loop", "after the other legs"):
         for _ in range(reps):
             static()
-            if order.startswith("after views"):
+            if order.startswith("after the other"):
                 other_legs()
             r.set_splat_overlap(True)
             ov = orbit_pass()
