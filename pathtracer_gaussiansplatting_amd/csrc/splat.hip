@@ -2307,7 +2307,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
   const uint32_t px = tile_x * GS_BLOCK_X + (wave & 1u) * 8u + (lane & 7u);
   const uint32_t py = tile_y * GS_BLOCK_Y + (wave >> 1) * 8u + (lane >> 3);
   const bool inside = px < cam.W && py < cam.H;
-  bool done = !inside;
+  // the wave's finished pixels as a lane mask in SGPRs (set: outside the image, saturated, or behind the mesh):
+  // the per-entry validity and the every-4-entries all-done test read it without moving it into a VGPR
+  unsigned long long done = __builtin_amdgcn_ballot_w64(!inside);
   const float pfx = (float)px, pfy = (float)py;
   const float ux = pfx - tx0, uy = pfy - ty0, uxx = ux * ux, uxy = ux * uy, uyy = uy * uy;
   const float lim = (OVER && inside) ? depth_lim[(size_t)py * cam.W + px] : 0.0f;
@@ -2322,7 +2324,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     // and every tile holds a pixel inside the image: a plain barrier instead of the counting one, which
     // reduces through LDS behind a second barrier.
     if (base == 0) __syncthreads();
-    else if (__syncthreads_count(done) == GS_BLOCK) break;
+    else if (__syncthreads_count(__builtin_amdgcn_inverse_ballot_w64(done)) == GS_BLOCK) break;
     const uint32_t idx = base + tid;
     if (!small) {
       if (idx < n) {
@@ -2364,9 +2366,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
     if (lane < 4) s_list[wave][cntu + lane] = GS_BLOCK * (uint32_t)sizeof(GStage);
     const uint32_t* list = s_list[wave];
     for (uint32_t j = 0; j < cntu; j += 4) {
-      // (the all-done test costs two VALU (the done mask from SGPRs to a compare): every
-      // GS_DONE_EVERY entries only)
-      if ((j & (GS_DONE_EVERY - 1u)) == 0u && __ballot(!done) == 0) break;
+      // (the all-done test every GS_DONE_EVERY entries: scalar, every lane of the wave is active here)
+      if ((j & (GS_DONE_EVERY - 1u)) == 0u && done == __builtin_amdgcn_read_exec()) break;
       const uint4 o4 = *reinterpret_cast<const uint4*>(list + j);  // 4 list entries
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -2376,7 +2377,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         const float cb = *reinterpret_cast<const float*>(stage + o + 32);
         if (OVER) {  // sorted by depth: the first Gaussian at or behind the mesh ends the pixel
           const float gd = *reinterpret_cast<const float*>(stage + o + 44);
-          done = done || !(gd < lim);
+          done |= __builtin_amdgcn_ballot_w64(!(gd < lim));
         }
         // z = A dx^2 + B dx dy + C dy^2 + log2 o as staged: a quadratic in the tile-local (ux, uy), five
         // FMAs (the centre-relative form costs seven; the expansion's rounding is ~1e-6 in z). (The
@@ -2384,15 +2385,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_BLEND_MIN_BLOCKS) void gs_sort_blend_k
         // so power <= 0 up to rounding at power ~ 0.)
         const float z = __builtin_fmaf(a.x, uxx, __builtin_fmaf(a.y, uxy, __builtin_fmaf(a.z, uyy,
                                        __builtin_fmaf(a.w, ux, __builtin_fmaf(b.x, uy, b.y)))));
-        const bool valid = !done && z >= -7.9943534f;  // alpha >= 1/255: z >= log2(1/255)
+        // alpha >= 1/255: z >= log2(1/255)
+        const bool valid = __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_ballot_w64(z >= -7.9943534f) & ~done);
         const float alpha = valid ? fminf(0.99f, __builtin_amdgcn_exp2f(z)) : 0.0f;
         float wgt = alpha * T;
         float test_T = T - wgt;
-        const bool term = test_T < 0.0001f;  // only a valid pair can get there
-        if (__ballot(term)) {  // rare: this Gaussian would saturate the pixel -> stop before it
-          done = done || term;
-          wgt = term ? 0.0f : wgt;
-          test_T = term ? T : test_T;
+        const unsigned long long term = __builtin_amdgcn_ballot_w64(test_T < 0.0001f);  // (only a valid pair)
+        if (term) {  // rare: this Gaussian would saturate the pixel -> stop before it
+          done |= term;
+          const bool t = __builtin_amdgcn_inverse_ballot_w64(term);
+          wgt = t ? 0.0f : wgt;
+          test_T = t ? T : test_T;
         }
         C0 = __builtin_fmaf(b.z, wgt, C0);
         C1 = __builtin_fmaf(b.w, wgt, C1);
