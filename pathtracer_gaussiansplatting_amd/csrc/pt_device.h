@@ -259,7 +259,8 @@ __device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, i
 struct Box4 {
   float tn[4];
   int c[4];
-  uint32_t hits;
+  unsigned long long hm[4];  // per child, the wave's lanes whose ray hits it (SGPR masks: the hit-count logic of
+                             // enter_box4 runs on the scalar unit instead of a per-lane count in VGPRs)
 };
 #if PTGS_PT_NEARFAR
 __device__ __forceinline__ float4 node_ld(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
@@ -282,7 +283,6 @@ __device__ __forceinline__ void box4(const Ray& r, const DevScene& sc, int node,
   const float NY[4] = {ny.x, ny.y, ny.z, ny.w}, FY[4] = {fy.x, fy.y, fy.z, fy.w};
   const float NZ[4] = {nz.x, nz.y, nz.z, nz.w}, FZ[4] = {fz.x, fz.y, fz.z, fz.w};
   const float CH[4] = {ch.x, ch.y, ch.z, ch.w};
-  o.hits = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float x0 = __builtin_fmaf(NX[j], r.inv.x, -r.oinv.x), x1 = __builtin_fmaf(FX[j], r.inv.x, -r.oinv.x);
@@ -299,7 +299,7 @@ __device__ __forceinline__ void box4(const Ray& r, const DevScene& sc, int node,
     const bool h = tn <= tf * 1.0000004f;
     o.tn[j] = h ? tn : __builtin_huge_valf();
     o.c[j] = f2i(CH[j]);
-    o.hits += h ? 1u : 0u;
+    o.hm[j] = __builtin_amdgcn_ballot_w64(h);
   }
 }
 #else
@@ -314,7 +314,6 @@ __device__ __forceinline__ void box4(const Ray& r, const DevScene& sc, int node,
   const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
   const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
   const float CH[4] = {ch.x, ch.y, ch.z, ch.w};
-  o.hits = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float x0 = __builtin_fmaf(LX[j], r.inv.x, -r.oinv.x), x1 = __builtin_fmaf(HX[j], r.inv.x, -r.oinv.x);
@@ -325,7 +324,7 @@ __device__ __forceinline__ void box4(const Ray& r, const DevScene& sc, int node,
     const bool h = tn <= tf * 1.0000004f;
     o.tn[j] = h ? tn : __builtin_huge_valf();
     o.c[j] = f2i(CH[j]);
-    o.hits += h ? 1u : 0u;
+    o.hm[j] = __builtin_amdgcn_ballot_w64(h);
   }
 }
 #endif
@@ -340,11 +339,14 @@ __device__ __forceinline__ void cswap4(Box4& b, int i, int j) {
 // children pushed farthest first; no hit child: pop().
 template <typename Push, typename Pop>
 __device__ __forceinline__ int enter_box4(Box4& b, Push push, Pop pop) {
-  if (b.hits == 0) return pop();
+  const unsigned long long h0 = b.hm[0], h1 = b.hm[1], h2 = b.hm[2], h3 = b.hm[3];
+  if (!__builtin_amdgcn_inverse_ballot_w64(h0 | h1 | h2 | h3)) return pop();
   cswap4(b, 0, 1); cswap4(b, 2, 3); cswap4(b, 0, 2); cswap4(b, 1, 3); cswap4(b, 1, 2);
-  if (b.hits > 3) push(b.c[3]);
-  if (b.hits > 2) push(b.c[2]);
-  if (b.hits > 1) push(b.c[1]);
+  // (the sorted hits come first: at least 4 / 3 / 2 of the four children hit, as lane masks)
+  const unsigned long long a01 = h0 & h1, o01 = h0 | h1, a23 = h2 & h3, o23 = h2 | h3;
+  if (__builtin_amdgcn_inverse_ballot_w64(a01 & a23)) push(b.c[3]);
+  if (__builtin_amdgcn_inverse_ballot_w64((a01 & o23) | (o01 & a23))) push(b.c[2]);
+  if (__builtin_amdgcn_inverse_ballot_w64(a01 | a23 | (o01 & o23))) push(b.c[1]);
   return b.c[0];
 }
 
@@ -385,7 +387,10 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
         leaf = node;
         node = pop();
       }
-      if (__all(leaf != DONE || node == DONE)) break;
+      // (every active lane holds a leaf or is done: the compares' lane mask against exec, no VGPR round trip)
+      if ((__builtin_amdgcn_ballot_w64(leaf != DONE) | __builtin_amdgcn_ballot_w64(node == DONE)) ==
+          __builtin_amdgcn_read_exec())
+        break;
     }
     if (leaf != DONE) {
       leaf_closest<STATS, TEX>(sc, r, leaf, h, seed, cnt);

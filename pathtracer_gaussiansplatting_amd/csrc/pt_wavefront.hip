@@ -258,7 +258,9 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_exte
         leaf = node;
         node = pop();
       }
-      if (__all(leaf != WF_DONE || node == WF_DONE)) break;
+      if ((__builtin_amdgcn_ballot_w64(leaf != WF_DONE) | __builtin_amdgcn_ballot_w64(node == WF_DONE)) ==
+          __builtin_amdgcn_read_exec())
+        break;
     }
     if (leaf != WF_DONE) {
       leaf_closest<STATS, TEX, PTGS_WF_AH_CALL_EXT>(sc, r, leaf, h, seed, tc);
