@@ -626,6 +626,15 @@ typedef struct ptgs_splat_buffers {
     uint32_t num_tiles;
 } ptgs_splat_buffers;
 int ptgs_splat_get_buffers(const ptgs_ctx* ctx, ptgs_splat_buffers* out);
+/* Debug/parity access to the most recent splat call's own pair rows when its front end was the fused
+ * one (every frame, published or not, timed or overlapped: the bench's frames): tile t's pairs are
+ * rows[t * row_capacity .. t * row_capacity + n_t), n_t = end - begin of tile_ranges[t] (the blend
+ * writes those ranges), each pair (depth bits << 32) | gaussian index, in no particular order (the blend
+ * sorts them in LDS; a tile's row may be left permuted). A tile with n_t > row_capacity kept its first
+ * row_capacity pairs only (completed through the spill pool). *rows = NULL, *row_capacity = 0 when that
+ * frame ran the three-launch front end. Device memory owned by the context, valid until the next splat
+ * call; synchronise the call's stream before reading. No reference counterpart (test access). */
+int ptgs_splat_get_tile_rows(const ptgs_ctx* ctx, const uint64_t** rows, uint32_t* row_capacity);
 
 /* With PTGS_FLAG_TIME_STAGES: milliseconds of the stages of the most recent ptgs_splat_gaussians
  * call, measured with hipEvents on its stream: [0] preprocess + count (tile histograms) [1] column

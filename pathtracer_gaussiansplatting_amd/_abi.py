@@ -204,6 +204,7 @@ SYMBOLS = {
     "ptgs_splat_gaussians_over": (_I, [_P, C.POINTER(Gaussians), C.POINTER(Ubo), _U, _U, _P, _P, _U, _U, _P,
                                        C.POINTER(SplatStats), _P]),
     "ptgs_splat_get_buffers": (_I, [_P, C.POINTER(SplatBuffers)]),
+    "ptgs_splat_get_tile_rows": (_I, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint32)]),
     "ptgs_splat_status_read": (_I, [_P, C.POINTER(SplatStatus), _P]),
     "ptgs_splat_reserve": (_I, [_P, _U]),
     "ptgs_gaussians_sort_spatial": (_I, [_P, C.POINTER(Gaussians), _P, _P, _P, _P, _P, _P, _P]),

@@ -1014,6 +1014,14 @@ int ptgs_splat_get_buffers(const ptgs_ctx* c, ptgs_splat_buffers* out) {
   return PTGS_OK;
 }
 
+int ptgs_splat_get_tile_rows(const ptgs_ctx* c, const uint64_t** rows, uint32_t* row_capacity) {
+  if (!c || !rows || !row_capacity) return PTGS_EINVAL;
+  const unsigned long long* r = nullptr;
+  splat_get_tile_rows(c->splat, &r, row_capacity);
+  *rows = (const uint64_t*)r;
+  return PTGS_OK;
+}
+
 int ptgs_splat_stage_ms(ptgs_ctx* c, float out_ms[6]) {
   if (!c || !out_ms) return PTGS_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));

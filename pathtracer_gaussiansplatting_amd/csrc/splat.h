@@ -68,6 +68,8 @@ uint32_t splat_pair_hint(const SplatWorkspace* w);
 // the latest frame's touched (workgroup, tile) runs and whether it ran the fused front end
 void splat_front_end_info(const SplatWorkspace* w, uint32_t* touched_runs, uint32_t* fused);
 void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out);
+// the latest frame's fused per-tile slot rows (its front end's unsorted keys) and their capacity (0: not fused)
+void splat_get_tile_rows(const SplatWorkspace* w, const unsigned long long** rows, uint32_t* cap);
 hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long** keys);
 
 // GLSL mat4 * mat4, column-major, fixed evaluation order ((a0*b0 + a1*b1) + a2*b2) + a3*b3

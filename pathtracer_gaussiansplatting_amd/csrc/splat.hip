@@ -73,6 +73,7 @@ struct SplatWorkspace {
   bool hint_recorded = false;
   hipEvent_t hint_event = nullptr;
   bool last_fused = false;    // the last frame ran the fused front end
+  uint32_t last_scap = 0;     // and its slot rows' capacity (ptgs_splat_get_tile_rows)
   uint32_t* k_host = nullptr;  // pinned, coherent [16]: K, largest tile, large tiles, -, touched runs,
                                // fused overflow, publishing path (1 fused / 2 three), -, spill demand,
                                // incomplete tile, bad ids, queued front-end slices, largest K (fused),
@@ -2960,6 +2961,7 @@ hipError_t splat_gaussians(SplatWorkspace* w, const ptgs_gaussians* g, const flo
     stats->fused = fused && !redone ? 1u : 0u;
   }
   w->last_fused = fused && !redone;
+  w->last_scap = w->last_fused ? scap : 0u;
   // the fused path sizes its rows from the largest tile of a finished frame: valid once the host has
   // seen one complete (a frame still in flight has not written its hint yet)
   if (!w->have_hint) {
@@ -3190,6 +3192,11 @@ void splat_get_buffers(const SplatWorkspace* w, ptgs_splat_buffers* out) {
   out->num_gaussians = w->last_n;
   out->num_rendered = w->last_k;
   out->num_tiles = w->last_tiles;
+}
+
+void splat_get_tile_rows(const SplatWorkspace* w, const unsigned long long** rows, uint32_t* cap) {
+  *rows = w->last_scap ? (const unsigned long long*)w->tile_slots.p : nullptr;
+  *cap = w->last_scap;
 }
 
 hipError_t splat_point_keys(SplatWorkspace* w, size_t npix, unsigned long long** keys) {

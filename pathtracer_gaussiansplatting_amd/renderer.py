@@ -320,6 +320,14 @@ class Renderer:
         self._chk(self.lib.ptgs_splat_get_buffers(self._h, C.byref(b)), "ptgs_splat_get_buffers")
         return b
 
+    def splat_tile_rows(self) -> tuple[int, int]:
+        """ptgs_splat_get_tile_rows: (device pointer, row capacity) of the latest splat's fused slot rows
+        (its front end's unsorted (depth bits << 32 | gaussian) pairs, tile t at t * capacity); (0, 0) when
+        that frame ran the three-launch front end."""
+        p, cap = C.c_void_p(), C.c_uint32()
+        self._chk(self.lib.ptgs_splat_get_tile_rows(self._h, C.byref(p), C.byref(cap)), "ptgs_splat_get_tile_rows")
+        return (p.value or 0), cap.value
+
     def splat_stage_ms(self) -> np.ndarray:
         """[preprocess+count, colscan, scatter, large-tile sort, 0, sort+blend] ms of the last splat
         (FLAG_TIME_STAGES)."""

@@ -6,7 +6,9 @@ through the same front ends, so the timed path's sorted keys / values / tile ran
 touched) are compared with the oracle's bit for bit: at the C2 headline (100k Gaussians, 1920x1080,
 Morton copy with ids, fused front end), at C4's 1M Gaussians (large-tile sorts), and over the edge cases
 of the suite (equal depths, tile-size boundaries, thin / faint Gaussians, a close camera). The published
-frame's pair count equals the timed frames' own count and its image equals theirs bit for bit."""
+frame's pair count equals the timed frames' own count and its image equals theirs bit for bit; the timed
+frames' own pairs are read back from their fused slot rows (ptgs_splat_get_tile_rows) and equal the
+oracle's per tile, serial and with frames in flight."""
 import numpy as np
 import pytest
 
@@ -29,6 +31,36 @@ def _read(renderer, ptr, n, dtype):
     return out
 
 
+def _check_timed_rows(r, ref):
+    """VERDICT r5 weak #1a: the timed frame's OWN pairs, read back from its fused slot rows
+    (ptgs_splat_get_tile_rows: unsorted (depth bits << 32 | gaussian) per tile, tile t at t * capacity, the
+    counts in the tile ranges the blend wrote). Per tile they must be the oracle's pairs as a set (the
+    blend's LDS sort orders them; that order is checked through the image). Returns the row capacity
+    (0: the frame ran three launches, nothing to read)."""
+    ptr, cap = r.splat_tile_rows()
+    if not cap:
+        return 0
+    b = r.splat_buffers()
+    tiles = b.num_tiles
+    rng = _read(r, b.tile_ranges, 2 * tiles, np.uint32).reshape(tiles, 2).astype(np.int64)
+    cnt = rng[:, 1] - rng[:, 0]
+    np.testing.assert_array_equal(rng[:, 0], np.arange(tiles, dtype=np.int64) * cap)
+    ref_rng = ref["ranges"].reshape(tiles, 2).astype(np.int64)
+    np.testing.assert_array_equal(cnt, ref_rng[:, 1] - ref_rng[:, 0])  # every tile's own pair count
+    assert cnt.max() <= cap, (cnt.max(), cap)  # (no tile spilled: its whole row is the frame's)
+    rows = _read(r, ptr, tiles * cap, np.uint64).reshape(tiles, cap)
+    got = rows[np.arange(cap)[None, :] < cnt[:, None]]  # tile-major
+    got_t = np.repeat(np.arange(tiles, dtype=np.uint64), cnt)
+    ref_keys = ref["keys"].astype(np.uint64)
+    want = ((ref_keys & np.uint64(0xFFFFFFFF)) << np.uint64(32)) | ref["vals"].astype(np.uint64)
+    want_t = ref_keys >> np.uint64(32)
+    np.testing.assert_array_equal(np.sort(got_t), want_t)
+    got = got[np.lexsort((got, got_t))]
+    want = want[np.lexsort((want, want_t))]
+    np.testing.assert_array_equal(got, want)
+    return cap
+
+
 def _check_tight(g, ubo, W, H, oracle_lib, frames=2, bg=(0.0, 0.0, 0.0), want_fused=None):
     """Timed frames (stream-ordered, Morton copy with ids) vs published tight frames vs the oracle's
     tight mode. Returns (K, fused) of the last published frame."""
@@ -49,6 +81,9 @@ def _check_tight(g, ubo, W, H, oracle_lib, frames=2, bg=(0.0, 0.0, 0.0), want_fu
         st_a = ra.splat_status()
         assert st_a.frames == 0 and st_a.incomplete_tiles == 0
         assert st_a.last_pairs == ref["K"], (st_a.last_pairs, ref["K"])  # the timed frames' own count
+        cap = _check_timed_rows(ra, ref)  # and their own pairs
+        if want_fused:
+            assert cap, "the timed frame did not run the fused front end"
         fused = []
         for k in range(frames):  # frame 0: three launches (sizes the rows); then the fused front end
             pub = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
@@ -117,6 +152,37 @@ def test_tight_binning_edge_cases(native_lib, oracle_lib, case):
         at = [0.0, 0.0, -8.0]
     ubo = make_ubo(Camera(aspect=W / H).look_at(eye, at), U.cornell(), 0)
     _check_tight(g, ubo, W, H, oracle_lib, bg=bg)
+
+
+def test_timed_rows_frames_in_flight_c2(native_lib, oracle_lib):
+    """The bench's headline frames (frames in flight, PTGS_FLAG_SPLAT_OVERLAP, ring of workspaces): after a
+    run of overlapped calls the latest call's own slot rows hold the oracle's pairs per tile, and its
+    image equals the oracle's within 1e-4."""
+    from pathtracer_gaussiansplatting_amd import Renderer
+    W, H = 1920, 1080
+    g = Y.gaussians_c2(100_000, seed=1)
+    ubo = make_ubo(Camera(aspect=W / H).look_at([0, 0, 0], [0, 0, -1]), U.cornell(), 0)
+    ref = oracle_lib.splat_gaussians(g, ubo, W, H, tight=True)
+    r = Renderer(0)
+    try:
+        d = r.sort_gaussians_spatial({k: _dev(v) for k, v in g.items()})
+        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        r.splat_gaussians(d, ubo, W, H, out)  # (sizes the rows)
+        torch.cuda.synchronize()
+        r.set_splat_overlap(True)
+        outs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(6)]
+        for o in outs:
+            r.splat_gaussians(d, ubo, W, H, o)
+        torch.cuda.synchronize()
+        assert _check_timed_rows(r, ref), "the overlapped frame did not run the fused front end"
+        for o in outs[1:]:
+            assert torch.equal(o, outs[0])
+        err = U.rel_l2(outs[-1].cpu().numpy(), ref["image"])
+        assert err < 1e-4, err
+        st = r.splat_status()
+        assert st.frames == 0 and st.incomplete_tiles == 0
+    finally:
+        r.close()
 
 
 @pytest.mark.parametrize("mode", ["rects", "tight"])
