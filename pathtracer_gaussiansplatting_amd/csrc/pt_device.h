@@ -69,7 +69,40 @@ struct TraversalCounters {
   uint32_t nodes;  // child-box tests
   uint32_t tris;   // ray-triangle tests
   uint32_t hits;   // closest hits (shaded surface points)
+#ifdef PT_LANES
+  struct PtLaneCounts* lanes_p;
+#endif
 };
+
+// PT_LANES builds (tools/pt_lanes.py, diagnostics only): per loop of the path tracer, how many times a wave
+// ran it and how many lanes were active in those runs (lane utilisation by phase). g_pt_lanes[2 i] wave
+// iterations, [2 i + 1] active lanes summed over them; i: PtLoop. Each work-item counts in registers and
+// adds its totals once at the end of the kernel (pt_lanes_flush).
+enum PtLoop { PT_L_NODE = 0, PT_L_LEAF, PT_L_TRI, PT_L_ANY_NODE, PT_L_ANY_TRI, PT_L_BOUNCE, PT_L_SAMPLE, PT_L_COUNT };
+#ifdef PT_LANES
+__device__ unsigned long long g_pt_lanes[2 * PT_L_COUNT];
+struct PtLaneCounts {
+  uint32_t w[PT_L_COUNT], l[PT_L_COUNT];
+};
+__device__ __forceinline__ void pt_lane_tick(PtLaneCounts& c, int i) {
+  const unsigned long long ex = __builtin_amdgcn_read_exec();
+  c.l[i] += 1u;
+  if (__lane_id() == (uint32_t)__builtin_ctzll(ex)) c.w[i] += 1u;
+}
+__device__ __forceinline__ void pt_lanes_flush(const PtLaneCounts& c) {
+  for (int i = 0; i < PT_L_COUNT; ++i) {
+    atomicAdd(&g_pt_lanes[2 * i], (unsigned long long)c.w[i]);
+    atomicAdd(&g_pt_lanes[2 * i + 1], (unsigned long long)c.l[i]);
+  }
+}
+#define PT_LANE_TICK(cnt, i) pt_lane_tick(*(cnt).lanes_p, (i))
+#define PT_LANES_INIT(tc) PtLaneCounts tc##_lanes = {}; (tc).lanes_p = &tc##_lanes
+#define PT_LANES_FLUSH(tc) pt_lanes_flush(tc##_lanes)
+#else
+#define PT_LANE_TICK(cnt, i) ((void)0)
+#define PT_LANES_INIT(tc) ((void)0)
+#define PT_LANES_FLUSH(tc) ((void)0)
+#endif
 
 // Traversal stack: PTGS_STACK entries per work-item in LDS, interleaved across the 256 work-items
 // of a workgroup (entry k of lane t at [k * 256 + t]: conflict-free ds_read/ds_write_b32).
@@ -229,6 +262,7 @@ __device__ __forceinline__ void leaf_closest(const DevScene& sc, const Ray& r, i
   // the next triangle's 48 B are in flight while this one is tested (+3%)
   float4 na = sc.tris[3u * start], nb = sc.tris[3u * start + 1u], nc = sc.tris[3u * start + 2u];
   for (uint32_t k = 0; k < count; ++k) {
+    PT_LANE_TICK(cnt, PT_L_TRI);
     float4 a = na, b = nb, c = nc;
     asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(b.x), "+v"(b.y), "+v"(b.z), "+v"(b.w),
                       "+v"(c.x), "+v"(c.y), "+v"(c.z), "+v"(c.w));
@@ -379,6 +413,7 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
   // (a register-cached stack top that hides the LDS read behind the node fetch measured -0.8%)
   for (;;) {
     while (node >= 0 && node != DONE) {
+      PT_LANE_TICK(cnt, PT_L_NODE);
       Box4 b;
       box4(r, sc, node, h.t, b);
       if (STATS) cnt.nodes += 4;
@@ -393,6 +428,7 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& sc, const Ray& r, u
         break;
     }
     if (leaf != DONE) {
+      PT_LANE_TICK(cnt, PT_L_LEAF);
       leaf_closest<STATS, TEX>(sc, r, leaf, h, seed, cnt);
       leaf = DONE;
     }
@@ -416,6 +452,7 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
   };
   while (true) {
     while (node >= 0) {
+      PT_LANE_TICK(cnt, PT_L_ANY_NODE);
       Box4 b;
       box4(r, sc, node, r.tmax, b);
       if (STATS) cnt.nodes += 4;
@@ -446,6 +483,7 @@ __device__ __forceinline__ bool trace_any(const DevScene& sc, const Ray& r, uint
     uint32_t start = L & 0x07ffffffu;
     uint32_t count = (L >> 27) + 1u;
     for (uint32_t k = 0; k < count; ++k) {
+      PT_LANE_TICK(cnt, PT_L_ANY_TRI);
       const float4* tp = sc.tris + 3u * (start + k);
       float4 a = tp[0], bb = tp[1], c = tp[2];
       if (STATS) cnt.tris++;

@@ -134,6 +134,7 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
   __shared__ int s_stack[PTGS_STACK * PTGS_PT_WG];
   ShadeCtx c; c.sc = &sc; c.cp = &cp; c.stack = s_stack + threadIdx.x; c.shadow_rays = 0;
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
+  PT_LANES_INIT(tc);
   uint32_t ext_rays = 0, samples = 0;
 
   const size_t pix = (size_t)y * W + x;
@@ -161,6 +162,7 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
     const uint32_t s = k * lpp + half;
     v3 acc = mk3(0.0f);
     if (active && s < spp) {
+      PT_LANE_TICK(tc, PT_L_SAMPLE);
       const uint32_t frame = frame0 + s * stride;
       v3 ro, rd;
       float4 blue;
@@ -176,6 +178,7 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
       p.color = mk3(0.0f); p.weight = mk3(1.0f); p.next_o = ro; p.next_d = rd;
       int max_depth = 12;
       for (int depth = 0; depth < max_depth; ++depth) {
+        PT_LANE_TICK(tc, PT_L_BOUNCE);
         p.depth = depth;
         Ray ray = make_ray(ro, rd, 0.001f, 10000.0f);
         ext_rays++;
@@ -226,6 +229,7 @@ __global__ __launch_bounds__(PTGS_PT_WG, PTGS_PT_MIN_WAVES) void pt_camera_kerne
     else accum[pix] = make_float4(state.x, state.y, state.z, 1.0f);
   }
   flush_counters(counters, ext_rays, c.shadow_rays, samples, tc, STATS);
+  PT_LANES_FLUSH(tc);
 #if !PTGS_PT_XCD_REMAP
   if (cost) {
     __syncthreads();  // (every wave of the tile is done)
@@ -255,6 +259,7 @@ __global__ __launch_bounds__(256, TEX ? 1 : PTGS_TORUS_MIN_WAVES) void pt_torus_
   __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
   ShadeCtx c; c.sc = &sc; c.cp = &cp; c.stack = s_stack + threadIdx.x; c.shadow_rays = 0;
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
+  PT_LANES_INIT(tc);
   uint32_t ext_rays = 0, nsamp = 0;
   if (index < n) {
     const uint32_t lx = index % side, ly = index / side;
@@ -354,6 +359,7 @@ __global__ __launch_bounds__(256) void pt_depth_kernel(DevScene sc, CamParams cp
   __shared__ int s_stack[PTGS_STACK * PTGS_BLOCK];
   if (x >= W || y >= row1) return;
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
+  PT_LANES_INIT(tc);
   const uint32_t seed = y * W + x + frame * 719393u;
   const float ux = ((float)x + 0.5f) / (float)W, uy = ((float)y + 0.5f) / (float)H;
   const float dx = ux * 2.0f - 1.0f, dy = uy * 2.0f - 1.0f;
@@ -510,6 +516,16 @@ hipError_t launch_pt_torus(const DevScene& sc, const CamParams& cp, const TorusP
 
 }  // namespace ptgs
 
+#ifdef PT_LANES
+// (diagnostic builds: the lane counts of pt_device.h PtLoop, read and cleared)
+extern "C" int ptgs_debug_pt_lanes(unsigned long long* host, unsigned int n) {
+  if (n > 2u * ptgs::PT_L_COUNT) n = 2u * ptgs::PT_L_COUNT;
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(ptgs::g_pt_lanes), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+  if (e) return (int)e;
+  static const unsigned long long zero[2 * ptgs::PT_L_COUNT] = {};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(ptgs::g_pt_lanes), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
 #ifdef PT_STAMP
 extern "C" int ptgs_debug_pt_stamps(unsigned long long* host, unsigned int n) {
   if (n > PT_STAMP_WG * 2u) n = PT_STAMP_WG * 2u;

@@ -219,6 +219,7 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_exte
   SlotStream ss;
   ss_init(ss, s_ring[threadIdx.x >> 6], begin, min(a.slots, begin + per_wave));
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
+  PT_LANES_INIT(tc);
   uint32_t traced = 0;
   bool active = false;
   uint32_t slot = 0, seed = 0;
@@ -417,6 +418,7 @@ __global__ __launch_bounds__(256, wf_min_waves(PTGS_WF_LDS_EXT)) void pt_wf_shad
   SlotStream ss;
   ss_init(ss, s_ring[threadIdx.x >> 6], begin, min(a.slots, begin + per_wave));
   TraversalCounters tc; tc.nodes = 0; tc.tris = 0; tc.hits = 0;
+  PT_LANES_INIT(tc);
   uint32_t traced = 0;
   bool active = false;
   uint32_t slot = 0, seed = 0;
